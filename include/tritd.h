@@ -1,0 +1,189 @@
+/*
+ * tritd.h — C ABI of libtritd.so, the MI355X-native TriTD-ADMM solver.
+ *
+ * Drop-in boundary for the reference call surface
+ *     [A,B,C,O,errHist] = triple_decomp_ADMM(D, r, opts)
+ * (fast_robust_triple_tensor/triple_decomp_ADMM.m:1, called at
+ *  traffic_triple_comparison.m:55 and — as triple_decomp_ADMM_outlier — at
+ *  video_triple_comparison.m:54), plus the L1 primitives the drivers and the
+ * north star name (triple_product.m:1, unfold.m:1, soft_threshold.m:1,
+ * buildF.m:1, buildG.m:1, buildH.m:1).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no framework types.
+ *  - All host arrays are MATLAB column-major: X(i,j,t) at i + n1*(j + n2*t).
+ *  - Factors use the reference shapes: A (n1,r,r), B (r,n2,r), C (r,r,n3).
+ *  - Functions named tritd_dev_* take DEVICE pointers and a hipStream_t
+ *    (passed as void*, NULL = default stream) and do not synchronise.
+ *  - Every function returns a tritd_status; on error the message is available
+ *    from tritd_last_error() (thread-local).
+ *  - Inputs are never written (MATLAB shares mxArrays copy-on-write).
+ */
+#ifndef TRITD_H
+#define TRITD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    TRITD_OK = 0,
+    TRITD_ERR_ARG = 1,         /* bad shape / pointer / mode (unfold.m:12 'Mode must be 1, 2, or 3.') */
+    TRITD_ERR_OPTS = 2,        /* missing opts field (triple_decomp_ADMM.m:16-20) */
+    TRITD_ERR_HIP = 3,         /* HIP runtime error */
+    TRITD_ERR_RCCL = 4,        /* RCCL error */
+    TRITD_ERR_NOMEM = 5,       /* device allocation failed */
+    TRITD_ERR_NODEV = 6,       /* no usable gfx950 device */
+    TRITD_ERR_UNSUPPORTED = 7, /* rank / dtype outside the built kernels */
+    TRITD_ERR_STATE = 8        /* call order / session state */
+} tritd_status;
+
+/* opts struct of triple_decomp_ADMM.m:16-20.  `present` is a bitmask of the
+ * TRITD_OPT_* fields the caller actually set; a missing required field is
+ * reported exactly like MATLAB's "Reference to non-existent field 'x'."
+ * Extra reference-driver fields (alphaA, alphaB, origin —
+ * traffic_triple_comparison.m:48-51) are ignored by the reference and have
+ * no slot here. */
+enum {
+    TRITD_OPT_MU = 1u << 0,
+    TRITD_OPT_RHO = 1u << 1,
+    TRITD_OPT_LAMBDA = 1u << 2,
+    TRITD_OPT_LAMBDA2 = 1u << 3,
+    TRITD_OPT_MAXITER = 1u << 4,
+    TRITD_OPT_TOL = 1u << 5,
+    TRITD_OPT_DISP = 1u << 6,
+    TRITD_OPT_ALL = 0x7fu
+};
+
+typedef struct {
+    double mu;        /* opts.mu      (muL = muO = mu, :16-17) */
+    double rho;       /* opts.rho     (rhoL = rhoO = rho) */
+    double lambda;    /* opts.lambda  (E soft-threshold weight, :47) */
+    double lambda2;   /* opts.lambda2 (ridge of update_A/update_B, :34-35) */
+    double tol;       /* opts.tol     (relative-change stop, :63) */
+    int32_t maxIter;  /* opts.maxIter */
+    int32_t disp;     /* opts.disp    (print every 10 iterations, :60-62) */
+    uint32_t present; /* TRITD_OPT_* bitmask */
+    uint32_t reserved;
+} tritd_opts;
+
+/* Line printer used for opts.disp ("Iter %d, errL=%.2e, errO=%.2e").
+ * Default: stdout.  MEX gateways install mexPrintf here. */
+typedef void (*tritd_print_fn)(const char* line, void* user);
+
+const char* tritd_version(void);
+const char* tritd_last_error(void);
+void tritd_set_print_callback(tritd_print_fn fn, void* user);
+/* Number of visible gfx950 devices (0 on a host without a GPU). */
+tritd_status tritd_device_count(int32_t* count);
+
+/* ---------------------------------------------------------------------------
+ * One-shot drop-in solver.
+ * Replaces fast_robust_triple_tensor/triple_decomp_ADMM.m:1-70.
+ *   D       : n1*n2*n3 doubles (host)
+ *   A0,B0,C0: initial factors in reference layout (the MATLAB wrapper draws
+ *             them with randn in the order of :23 so the RNG stream matches)
+ *   A,B,C   : outputs, reference layout
+ *   O, E    : outputs, n1*n2*n3 (E is the 6th, extra output; may be NULL)
+ *   errHist : capacity maxIter; *iters receives k (errHist = errHist(1:k), :68)
+ * Runs on `device` (-1 = current/0).
+ * ------------------------------------------------------------------------- */
+tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                            const tritd_opts* opts, const double* A0, const double* B0,
+                            const double* C0, double* A, double* B, double* C, double* O,
+                            double* E, double* errHist, int32_t* iters, int32_t device);
+
+/* ---------------------------------------------------------------------------
+ * Sessions: the device-resident ADMM loop, steppable (bench), shardable
+ * along mode 1 (multi-GPU).  A session owns a shard i in [i0, i1) of the
+ * global n1 x n2 x n3 problem (i0 = 0, i1 = n1 for one GPU).
+ * ------------------------------------------------------------------------- */
+typedef struct tritd_session tritd_session;
+typedef struct tritd_comm tritd_comm;
+
+enum {
+    TRITD_SESSION_D_ON_DEVICE = 1 /* D is a device pointer on `device` */
+};
+
+/* D points at D(i0,0,0); consecutive (j,t) fibres are ldD elements apart
+ * (ldD = n1 for a full column-major tensor).  A0 is the FULL (n1,r,r)
+ * initial A (rows i0..i1-1 are used); B0, C0 are full.  comm = NULL for a
+ * single process/GPU. */
+tritd_status tritd_session_create(tritd_session** out, int32_t device, const double* D, int64_t ldD,
+                                  int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1,
+                                  int32_t r, const tritd_opts* opts, const double* A0,
+                                  const double* B0, const double* C0, tritd_comm* comm,
+                                  uint32_t flags);
+/* Enqueue `iters` ADMM iterations (no host synchronisation unless opts.disp).
+ * Iterations after the stop test of :63 fires, or beyond maxIter, are no-ops. */
+tritd_status tritd_session_run(tritd_session* s, int32_t iters);
+/* Wait for the enqueued work; report iterations completed and the stop flag. */
+tritd_status tritd_session_sync(tritd_session* s, int32_t* iters_done, int32_t* stopped);
+/* Copy results to the host.  A: full (n1,r,r) buffer, only rows i0..i1-1 are
+ * written; B, C full; O, E: the shard, leading dimension ldOE (>= i1-i0);
+ * errHist capacity maxIter.  Any pointer may be NULL. */
+tritd_status tritd_session_get(tritd_session* s, double* A, double* B, double* C, double* O,
+                               double* E, int64_t ldOE, double* errHist, int32_t* iters);
+/* Driver RRE (traffic_triple_comparison.m:62-63,194-199) of the current
+ * factors against a device-resident reference tensor X (same shard/ld as D):
+ *   sum over the shard of (triple_product(A,B,C) - X)^2 and of X^2.
+ * (Combine across ranks, then RRE = sqrt(num/den).) */
+tritd_status tritd_session_rre_parts(tritd_session* s, const double* dX, int64_t ldX, double* num,
+                                     double* den);
+/* Kernel-level timing of the dominant kernels over the last run (ms per
+ * launch, HIP events on the session stream; 0 when timing is disabled). */
+tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable);
+tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, double* mode3_ms,
+                                     double* iteration_ms, int32_t* samples);
+void tritd_session_destroy(tritd_session* s);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU: one process per GPU, RCCL over xGMI.  Rank 0 creates the id,
+ * the host side broadcasts its 128 bytes (e.g. torch.distributed), every
+ * rank calls tritd_comm_create.
+ * ------------------------------------------------------------------------- */
+tritd_status tritd_comm_unique_id(void* id128);
+tritd_status tritd_comm_create(tritd_comm** out, const void* id128, int32_t nranks, int32_t rank,
+                               int32_t device);
+void tritd_comm_destroy(tritd_comm* c);
+
+/* Single-GPU rehearsal of the sharded path: `nshards` sessions on one device
+ * whose all-reduces are summed on the device in shard order.  Used by the
+ * parity tests to check the mode-1 sharding on a 1-GPU box. */
+tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
+                                            int32_t r, const tritd_opts* opts, const double* A0,
+                                            const double* B0, const double* C0, int32_t nshards,
+                                            double* A, double* B, double* C, double* O, double* E,
+                                            double* errHist, int32_t* iters, int32_t device);
+
+/* ---------------------------------------------------------------------------
+ * Primitives (host pointers).  Each replaces the named reference file.
+ * ------------------------------------------------------------------------- */
+/* triple_product.m:1-7: X = reshape(unfold(A,1)*buildF(B,C), n1,n2,n3). */
+tritd_status tritd_triple_product_f64(const double* A, const double* B, const double* C, int64_t n1,
+                                      int64_t n2, int64_t n3, int32_t r, double* X);
+/* unfold.m:1-13: mode 1 reshape, mode 2 permute [2 1 3], mode 3 permute [3 1 2]. */
+tritd_status tritd_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t mode,
+                              double* Xn);
+/* soft_threshold.m:1-2: sign(X).*max(abs(X)-lam,0), n elements. */
+tritd_status tritd_soft_threshold_f64(const double* X, int64_t n, double lam, double* Y);
+/* buildF.m / buildG.m / buildH.m.  which = 'F' (P=B (r,n2,r), Q=C (r,r,n3)),
+ * 'G' (P=A (n1,r,r), Q=C), 'H' (P=A, Q=B (r,n2,r)).  out: r^2 x (nP*nQ). */
+tritd_status tritd_build_design_f64(char which, const double* P, const double* Q, int64_t nP,
+                                    int64_t nQ, int32_t r, double* out);
+
+/* Device-pointer variants (for device-resident callers and the bench). */
+tritd_status tritd_dev_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t mode,
+                                  double* Xn, void* stream);
+tritd_status tritd_dev_soft_threshold_f64(const double* X, int64_t n, double lam, double* Y,
+                                          void* stream);
+tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, const double* C,
+                                          int64_t n1, int64_t n2, int64_t n3, int32_t r, double* X,
+                                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRITD_H */

@@ -1,0 +1,71 @@
+"""Generate the committed golden vectors under tests/golden/.
+
+The reference is MATLAB-only and MATLAB/Octave are absent here (SURVEY.md
+§8c), so the vectors come from the numpy restatement in
+`oracle/tritd_oracle.py` (itself pinned against the reference's own loop
+definitions, tests/test_oracle.py).  Run from the repo root:
+
+    python tests/golden/make_golden.py
+
+Each .npz holds inputs (D, A0, B0, C0, r, opts as JSON) and outputs
+(A, B, C, O, E, errHist, k), plus the state after iterations 1 and 2 for the
+small cases (to localise a divergence).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd"))
+
+import tritd_oracle as orc  # noqa: E402
+from tritd import synth  # noqa: E402
+
+CASES = {
+    # name: (generator, kwargs, r, opts, keep full trace?)
+    "g12x10x8_r2": (synth.low_rank_plus_outliers, dict(n1=12, n2=10, n3=8, r=2), 2,
+                    dict(synth.TRAFFIC_OPTS, maxIter=30), True),
+    "g30_r3": (synth.low_rank_plus_outliers, dict(n1=30, n2=30, n3=30, r=3), 3,
+               dict(synth.TRAFFIC_OPTS), False),
+    "g54x4x96_r5_sensor": (synth.sensor_like, dict(n1=54, n2=4, n3=96, r=5), 5,
+                           dict(synth.TRAFFIC_OPTS), False),
+    "g20x24x18_r5_video": (synth.video_like, dict(n1=20, n2=24, n3=18, r=5), 5,
+                           dict(synth.VIDEO_OPTS, maxIter=40), False),
+    # a large tol makes the stop test at :63 fire early (errHist truncation)
+    "g12x10x8_r2_stop": (synth.low_rank_plus_outliers, dict(n1=12, n2=10, n3=8, r=2), 2,
+                         dict(synth.TRAFFIC_OPTS, tol=0.2), False),
+    # r=8 exercises the R=64 (full MFMA tile) code path at a small size
+    "g17x16x20_r8": (synth.low_rank_plus_outliers, dict(n1=17, n2=16, n3=20, r=8), 8,
+                     dict(synth.TRAFFIC_OPTS, maxIter=25), False),
+}
+
+
+def make(name):
+    gen, kw, r, opts, full = CASES[name]
+    d = gen(**kw)
+    res = orc.triple_decomp_ADMM(d["D"], r, opts, d["A0"], d["B0"], d["C0"], trace_iters=(1, 2))
+    A, B, C, O, eh, E, k, trace = res
+    out = dict(D=d["D"], A0=d["A0"], B0=d["B0"], C0=d["C0"], r=np.int64(r),
+               opts=np.array(json.dumps(opts)), A=A, B=B, C=C, O=O, E=E, errHist=eh, k=np.int64(k))
+    if "Lstar" in d:
+        out["Lstar"] = d["Lstar"]
+    for it in (1, 2):
+        st = trace[it]
+        for key in ("A", "B", "C"):
+            out[f"it{it}_{key}"] = st[key]
+        if full:
+            for key in ("O", "E", "Y_L", "Y_O"):
+                out[f"it{it}_{key}"] = st[key]
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    return k, eh[-1]
+
+
+if __name__ == "__main__":
+    for n in CASES:
+        print(n, *make(n))

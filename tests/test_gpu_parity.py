@@ -1,0 +1,164 @@
+"""GPU parity: libtritd (HIP, gfx950) against the oracle on the same inputs.
+
+Tolerances (fp64; BASELINE.json north_star "within a stated fp64 tolerance"):
+  * L = triple_product(A,B,C), O, E : relative Frobenius <= 1e-9
+  * A, B, C                         : relative Frobenius <= 1e-8
+  * errHist                         : |d| <= 1e-8*errHist + 1e-13 entrywise, same k
+    (errHist is ||resL||/||D|| + ||resO||/||D||; resL = D - L - O cancels, so
+    its rounding floor is ~eps in units of ||D||, hence the absolute floor)
+  * data-movement primitives (unfold, buildF/G/H, soft_threshold): bit-exact
+The GPU and the oracle differ only in summation order and in inverse-vs-pinv
+of well-conditioned R x R Grams (<= 1.4e-11 after 100 its).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden, rel
+
+pytestmark = pytest.mark.gpu
+
+TOL_LOE = 1e-9
+TOL_ABC = 1e-8
+TOL_ERR = 1e-8
+ATOL_ERR = 1e-13
+
+
+@pytest.fixture(scope="module")
+def tritd():
+    import tritd as t
+    assert t.device_count() > 0, "no GPU visible: the HIP path must run, there is no CPU fallback"
+    return t
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import tritd_oracle
+    return tritd_oracle
+
+
+def check_solution(orc, got, ref, k_ref):
+    A, B, C, O, eh, E, k = got
+    assert k == k_ref
+    assert len(eh) == k_ref
+    L = orc.triple_product(A, B, C)
+    Lr = orc.triple_product(ref["A"], ref["B"], ref["C"])
+    assert rel(L, Lr) <= TOL_LOE
+    assert rel(O, ref["O"]) <= TOL_LOE
+    assert rel(E, ref["E"]) <= TOL_LOE
+    for key, X in (("A", A), ("B", B), ("C", C)):
+        assert rel(X, ref[key]) <= TOL_ABC, key
+    np.testing.assert_allclose(eh, ref["errHist"], rtol=TOL_ERR, atol=ATOL_ERR)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_admm_matches_golden(tritd, orc, name):
+    g = load_golden(name)
+    got = tritd.triple_decomp_ADMM(g["D"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                   return_E=True, return_iters=True)
+    check_solution(orc, got, g, g["k"])
+
+
+@pytest.mark.parametrize("name", ["g12x10x8_r2", "g30_r3", "g17x16x20_r8"])
+def test_admm_first_iterations(tritd, orc, name):
+    """State after iterations 1 and 2 (localises a divergence)."""
+    g = load_golden(name)
+    for it in (1, 2):
+        opts = dict(g["opts"], maxIter=it)
+        A, B, C, O, eh, k = tritd.triple_decomp_ADMM(g["D"], g["r"], opts, g["A0"], g["B0"], g["C0"],
+                                                     return_iters=True)
+        assert k == it
+        for key, X in (("A", A), ("B", B), ("C", C)):
+            assert rel(X, g[f"it{it}_{key}"]) <= 1e-11, (it, key)
+
+
+@pytest.mark.parametrize("name,P", [("g30_r3", 2), ("g30_r3", 3), ("g54x4x96_r5_sensor", 4),
+                                    ("g17x16x20_r8", 2)])
+def test_virtual_shards_match_golden(tritd, orc, name, P):
+    """Mode-1 sharded schedule rehearsed as P shards on one GPU."""
+    g = load_golden(name)
+    got = tritd.triple_decomp_ADMM(g["D"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                   return_E=True, return_iters=True, virtual_shards=P)
+    check_solution(orc, got, g, g["k"])
+
+
+def test_medium_against_oracle(tritd, orc):
+    """A size with several workgroups per kernel and ragged padding."""
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(70, 33, 50, 8, seed=3)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=6)
+    ref = orc.triple_decomp_ADMM(d["D"], 8, opts, d["A0"], d["B0"], d["C0"])
+    got = tritd.triple_decomp_ADMM(d["D"], 8, opts, d["A0"], d["B0"], d["C0"], return_E=True,
+                                   return_iters=True)
+    A, B, C, O, eh, E, k = got
+    assert k == ref[6]
+    assert rel(O, ref[3]) <= TOL_LOE
+    assert rel(E, ref[5]) <= TOL_LOE
+    np.testing.assert_allclose(eh, ref[4], rtol=TOL_ERR, atol=ATOL_ERR)
+
+
+def test_disp_prints_like_reference(tritd, orc):
+    g = load_golden("g30_r3")
+    opts = dict(g["opts"], disp=1, maxIter=20)
+    lines = []
+    tritd.set_printer(lines.append)
+    try:
+        tritd.triple_decomp_ADMM(g["D"], g["r"], opts, g["A0"], g["B0"], g["C0"])
+    finally:
+        tritd.set_printer(None)
+    ref_lines = []
+    orc.triple_decomp_ADMM(g["D"], g["r"], opts, g["A0"], g["B0"], g["C0"], printer=ref_lines.append)
+    assert [l.split(",")[0] for l in lines] == [l.split(",")[0] for l in ref_lines] == ["Iter 10", "Iter 20"]
+    assert lines == ref_lines
+
+
+def test_maxiter_zero_returns_initial_factors(tritd):
+    g = load_golden("g12x10x8_r2")
+    A, B, C, O, eh = tritd.triple_decomp_ADMM(g["D"], g["r"], dict(g["opts"], maxIter=0),
+                                              g["A0"], g["B0"], g["C0"])
+    assert eh.size == 0
+    np.testing.assert_array_equal(A, g["A0"])
+    np.testing.assert_array_equal(B, g["B0"])
+    np.testing.assert_array_equal(C, g["C0"])
+    assert not O.any()
+
+
+# ---------------------------------------------------------------------------
+# primitives
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("shape", [(12, 10, 8), (30, 30, 30), (65, 3, 130), (1, 7, 1), (128, 64, 2)])
+def test_unfold_bit_exact(tritd, orc, shape):
+    X = np.asfortranarray(np.random.default_rng(1).standard_normal(shape))
+    for mode in (1, 2, 3):
+        np.testing.assert_array_equal(tritd.unfold(X, mode), orc.unfold(X, mode))
+
+
+def test_unfold_bad_mode(tritd):
+    with pytest.raises(tritd.TritdError, match="Mode must be 1, 2, or 3."):
+        tritd.unfold(np.zeros((2, 2, 2)), 0)
+
+
+def test_soft_threshold_bit_exact(tritd, orc):
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal(10001) * 3
+    X[:6] = [0.0, -0.0, np.nan, np.inf, -np.inf, 1.8]
+    for lam in (0.0, 1.8, 1e-4):
+        got = tritd.soft_threshold(X, lam)
+        np.testing.assert_array_equal(got, orc.soft_threshold(X, lam))
+
+
+@pytest.mark.parametrize("n1,n2,n3,r", [(12, 10, 8, 2), (30, 31, 29, 3), (17, 16, 20, 8), (5, 4, 33, 5)])
+def test_triple_product(tritd, orc, n1, n2, n3, r):
+    from tritd import synth
+    A, B, C = synth.random_factors(n1, n2, n3, r, seed=n1)
+    got = tritd.triple_product(A, B, C)
+    ref = orc.triple_product_loops(A, B, C) if n1 * n2 * n3 * r * r < 200000 else orc.triple_product(A, B, C)
+    assert rel(got, ref) <= 1e-13
+
+
+@pytest.mark.parametrize("r", [2, 3, 5])
+def test_design_matrices_bit_exact(tritd, orc, r):
+    from tritd import synth
+    A, B, C = synth.random_factors(9, 7, 6, r, seed=r)
+    np.testing.assert_array_equal(tritd.buildF(B, C), orc.buildF(B, C))
+    np.testing.assert_array_equal(tritd.buildG(A, C), orc.buildG(A, C))
+    np.testing.assert_array_equal(tritd.buildH(A, B), orc.buildH(A, B))

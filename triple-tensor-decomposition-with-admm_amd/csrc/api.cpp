@@ -1,0 +1,434 @@
+// C ABI of libtritd.so (include/tritd.h).  Every entry point validates its
+// arguments the way the reference fails (missing opts field, bad unfold
+// mode, >3-D data), converts exceptions into tritd_status + a thread-local
+// message, and never writes its inputs.
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "solver.h"
+
+using namespace tritd;
+
+namespace {
+thread_local std::string g_last_error;
+tritd_print_fn g_print = nullptr;
+void* g_print_user = nullptr;
+std::mutex g_mutex;  // calls are not re-entrant (SURVEY.md §8b Threading)
+
+tritd_status fail(tritd_status s, const std::string& m) {
+    g_last_error = m;
+    return s;
+}
+
+template <class F>
+tritd_status guarded(F&& f) {
+    try {
+        f();
+        g_last_error.clear();
+        return TRITD_OK;
+    } catch (const Error& e) {
+        return fail(e.code, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(TRITD_ERR_NOMEM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(TRITD_ERR_HIP, e.what());
+    }
+}
+
+void check_opts(const tritd_opts* o) {
+    if (!o) throw Error(TRITD_ERR_OPTS, "opts is NULL");
+    // triple_decomp_ADMM.m:16-20 reads the fields in this order
+    static const struct {
+        uint32_t bit;
+        const char* name;
+    } fields[] = {{TRITD_OPT_MU, "mu"},         {TRITD_OPT_RHO, "rho"},   {TRITD_OPT_LAMBDA, "lambda"},
+                  {TRITD_OPT_LAMBDA2, "lambda2"}, {TRITD_OPT_MAXITER, "maxIter"},
+                  {TRITD_OPT_TOL, "tol"},       {TRITD_OPT_DISP, "disp"}};
+    for (const auto& f : fields)
+        if (!(o->present & f.bit))
+            throw Error(TRITD_ERR_OPTS, std::string("Reference to non-existent field '") + f.name + "'.");
+}
+
+tritd_opts normalized(const tritd_opts* o) {
+    tritd_opts c = *o;
+    if (c.maxIter < 0) c.maxIter = 0;  // for k = 1:maxIter runs zero times
+    return c;
+}
+
+void check_dims(int64_t n1, int64_t n2, int64_t n3, int32_t r) {
+    if (n1 <= 0 || n2 <= 0 || n3 <= 0) throw Error(TRITD_ERR_ARG, "tensor dimensions must be positive");
+    if (r <= 0) throw Error(TRITD_ERR_ARG, "rank r must be positive");
+    if (r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "fp64 path supports r <= 8 (R = r^2 <= 64)");
+}
+
+void need(const void* p, const char* what) {
+    if (!p) throw Error(TRITD_ERR_ARG, std::string(what) + " is NULL");
+}
+
+int pick_device(int32_t device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        throw Error(TRITD_ERR_NODEV, "no HIP device visible (libtritd has no CPU fallback)");
+    int d = device;
+    if (d < 0) TRITD_HIP(hipGetDevice(&d));
+    if (d >= n) throw Error(TRITD_ERR_NODEV, "device index out of range");
+    hipDeviceProp_t prop;
+    TRITD_HIP(hipGetDeviceProperties(&prop, d));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        throw Error(TRITD_ERR_NODEV, std::string("libtritd is built for gfx950, device is ") + prop.gcnArchName);
+    TRITD_HIP(hipSetDevice(d));
+    return d;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace
+
+namespace tritd {
+void emit_line(const char* line) {
+    if (g_print) {
+        g_print(line, g_print_user);
+    } else {
+        std::printf("%s\n", line);
+        std::fflush(stdout);
+    }
+}
+}  // namespace tritd
+
+extern "C" {
+
+const char* tritd_version(void) { return "tritd-mi355x 0.1.0 (gfx950, fp64)"; }
+const char* tritd_last_error(void) { return g_last_error.c_str(); }
+
+void tritd_set_print_callback(tritd_print_fn fn, void* user) {
+    g_print = fn;
+    g_print_user = user;
+}
+
+tritd_status tritd_device_count(int32_t* count) {
+    return guarded([&] {
+        need(count, "count");
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        *count = n;
+    });
+}
+
+tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                            const tritd_opts* opts, const double* A0, const double* B0,
+                            const double* C0, double* A, double* B, double* C, double* O,
+                            double* E, double* errHist, int32_t* iters, int32_t device) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        check_opts(opts);
+        check_dims(n1, n2, n3, r);
+        need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        const int dev = pick_device(device);
+        const tritd_opts o = normalized(opts);
+        Session s(dev, D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, 0);
+        s.run(o.maxIter);
+        int k = 0;
+        s.get(A, B, C, O, E, n1, errHist, &k);
+        if (iters) *iters = k;
+    });
+}
+
+tritd_status tritd_session_create(tritd_session** out, int32_t device, const double* D, int64_t ldD,
+                                  int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1,
+                                  int32_t r, const tritd_opts* opts, const double* A0,
+                                  const double* B0, const double* C0, tritd_comm* comm,
+                                  uint32_t flags) {
+    return guarded([&] {
+        need(out, "out");
+        *out = nullptr;
+        check_opts(opts);
+        check_dims(n1, n2, n3, r);
+        need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        if (i0 < 0 || i1 > n1 || i0 >= i1) throw Error(TRITD_ERR_ARG, "bad shard range");
+        if (ldD < i1 - i0) throw Error(TRITD_ERR_ARG, "ldD smaller than the shard");
+        const int dev = pick_device(device);
+        auto* s = new Session(dev, D, ldD, n1, n2, n3, i0, i1, r, normalized(opts), A0, B0, C0,
+                              comm, flags);
+        *out = reinterpret_cast<tritd_session*>(s);
+    });
+}
+
+tritd_status tritd_session_run(tritd_session* s, int32_t iters) {
+    return guarded([&] {
+        need(s, "session");
+        reinterpret_cast<Session*>(s)->run(iters);
+    });
+}
+
+tritd_status tritd_session_sync(tritd_session* s, int32_t* iters_done, int32_t* stopped) {
+    return guarded([&] {
+        need(s, "session");
+        int d = 0, st = 0;
+        reinterpret_cast<Session*>(s)->sync(&d, &st);
+        if (iters_done) *iters_done = d;
+        if (stopped) *stopped = st;
+    });
+}
+
+tritd_status tritd_session_get(tritd_session* s, double* A, double* B, double* C, double* O,
+                               double* E, int64_t ldOE, double* errHist, int32_t* iters) {
+    return guarded([&] {
+        need(s, "session");
+        auto* S = reinterpret_cast<Session*>(s);
+        if ((O || E) && ldOE < S->geom().n1l) throw Error(TRITD_ERR_ARG, "ldOE smaller than the shard");
+        int k = 0;
+        S->get(A, B, C, O, E, ldOE, errHist, &k);
+        if (iters) *iters = k;
+    });
+}
+
+tritd_status tritd_session_rre_parts(tritd_session* s, const double* dX, int64_t ldX, double* num,
+                                     double* den) {
+    return guarded([&] {
+        need(s, "session"); need(dX, "X"); need(num, "num"); need(den, "den");
+        reinterpret_cast<Session*>(s)->rre_parts(dX, ldX, num, den);
+    });
+}
+
+tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable) {
+    return guarded([&] {
+        need(s, "session");
+        reinterpret_cast<Session*>(s)->set_timing(enable != 0);
+    });
+}
+
+tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, double* mode3_ms,
+                                     double* iteration_ms, int32_t* samples) {
+    return guarded([&] {
+        need(s, "session");
+        int n = 0;
+        reinterpret_cast<Session*>(s)->kernel_ms(fused_update_ms, mode3_ms, iteration_ms, &n);
+        if (samples) *samples = n;
+    });
+}
+
+void tritd_session_destroy(tritd_session* s) { delete reinterpret_cast<Session*>(s); }
+
+tritd_status tritd_comm_unique_id(void* id128) {
+    return guarded([&] {
+        need(id128, "id");
+        ncclUniqueId id;
+        const ncclResult_t r = ncclGetUniqueId(&id);
+        if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, ncclGetErrorString(r));
+        std::memcpy(id128, &id, sizeof id);
+    });
+}
+
+tritd_status tritd_comm_create(tritd_comm** out, const void* id128, int32_t nranks, int32_t rank,
+                               int32_t device) {
+    return guarded([&] {
+        need(out, "out"); need(id128, "id");
+        *out = nullptr;
+        if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(TRITD_ERR_ARG, "bad rank/nranks");
+        const int dev = pick_device(device);
+        auto c = std::make_unique<tritd_comm>();
+        c->nranks = nranks;
+        c->rank = rank;
+        c->device = dev;
+        ncclUniqueId id;
+        std::memcpy(&id, id128, sizeof id);
+        const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+        if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        *out = c.release();
+    });
+}
+
+void tritd_comm_destroy(tritd_comm* c) {
+    if (!c) return;
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+}
+
+tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
+                                            int32_t r, const tritd_opts* opts, const double* A0,
+                                            const double* B0, const double* C0, int32_t nshards,
+                                            double* A, double* B, double* C, double* O, double* E,
+                                            double* errHist, int32_t* iters, int32_t device) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        check_opts(opts);
+        check_dims(n1, n2, n3, r);
+        need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        if (nshards < 1 || nshards > 16 || nshards > n1) throw Error(TRITD_ERR_ARG, "nshards must be in 1..min(16,n1)");
+        const int dev = pick_device(device);
+        const tritd_opts o = normalized(opts);
+        hipStream_t st;
+        TRITD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        struct StreamGuard {
+            hipStream_t s;
+            ~StreamGuard() { (void)hipStreamDestroy(s); }
+        } sg{st};
+        std::vector<std::unique_ptr<Session>> ss;
+        const int64_t chunk = (n1 + nshards - 1) / nshards;
+        for (int p = 0; p < nshards; ++p) {
+            const int64_t i0 = p * chunk, i1 = std::min<int64_t>(n1, i0 + chunk);
+            if (i0 >= i1) break;
+            ss.emplace_back(new Session(dev, D + i0, n1, n1, n2, n3, i0, i1, r, o, A0, B0, C0, nullptr,
+                                        0, st, /*defer_normD=*/true));
+        }
+        const int P = (int)ss.size();
+        std::vector<double*> b(P);
+        auto vsum = [&](double* (Session::*get)(), int64_t count) {
+            for (int p = 0; p < P; ++p) b[p] = ((*ss[p]).*get)();
+            launch_vsum(b.data(), P, count, st);
+        };
+        vsum(&Session::red3, 2);
+        for (auto& s : ss) s->set_normD_from_red3();
+        for (int it = 0; it < o.maxIter; ++it) {
+            int k = 0;
+            for (auto& s : ss) k = s->next_iter();
+            if (!k) break;
+            for (auto& s : ss) s->phaseA(k);
+            vsum(&Session::red1, ss[0]->red1_count());
+            for (auto& s : ss) s->phaseB(k);
+            vsum(&Session::red2, ss[0]->red2_count());
+            for (auto& s : ss) s->phaseC(k);
+            vsum(&Session::red3, 2);
+            for (auto& s : ss) s->phaseD(k);
+            ss[0]->maybe_print(k);
+        }
+        int k = 0;
+        for (int p = 0; p < P; ++p) {
+            const int64_t i0 = ss[p]->geom().i0;
+            ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, O ? O + i0 : nullptr,
+                       E ? E + i0 : nullptr, n1, p == 0 ? errHist : nullptr, &k);
+        }
+        if (iters) *iters = k;
+    });
+}
+
+// ---------------------------------------------------------------------------
+// primitives
+// ---------------------------------------------------------------------------
+tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, const double* C,
+                                          int64_t n1, int64_t n2, int64_t n3, int32_t r, double* X,
+                                          void* stream) {
+    return guarded([&] {
+        check_dims(n1, n2, n3, r);
+        need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
+        hipStream_t st = as_stream(stream);
+        const Geom g = make_geom(n1, n2, n3, 0, n1, r);
+        const int64_t R = (int64_t)r * r;
+        std::vector<double> hA(n1 * R), hB(R * n2), hC(R * n3);
+        TRITD_HIP(hipMemcpyAsync(hA.data(), A, hA.size() * 8, hipMemcpyDeviceToHost, st));
+        TRITD_HIP(hipMemcpyAsync(hB.data(), B, hB.size() * 8, hipMemcpyDeviceToHost, st));
+        TRITD_HIP(hipMemcpyAsync(hC.data(), C, hC.size() * 8, hipMemcpyDeviceToHost, st));
+        TRITD_HIP(hipStreamSynchronize(st));
+        std::vector<double> Ah, AhT, Bh, Ch, ChT;
+        pack_A(g, hA.data(), Ah, AhT);
+        pack_B(g, hB.data(), Bh);
+        pack_C(g, hC.data(), Ch, ChT);
+        DBuf dAh, dBh, dChT, L;
+        dAh.alloc(Ah.size()); dBh.alloc(Bh.size()); dChT.alloc(ChT.size());
+        TRITD_HIP(hipMemcpy(dAh.p, Ah.data(), Ah.size() * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dBh.p, Bh.data(), Bh.size() * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dChT.p, ChT.data(), ChT.size() * 8, hipMemcpyHostToDevice));
+        L.alloc((size_t)g.Np);
+        launch_tp(g, dAh.p, dBh.p, dChT.p, L.p, nullptr, nullptr, 0, st);
+        TRITD_HIP(hipMemcpy2DAsync(X, n1 * 8, L.p, g.n1p * 8, n1 * 8, (size_t)(n2 * n3),
+                                   hipMemcpyDeviceToDevice, st));
+        TRITD_HIP(hipStreamSynchronize(st));
+    });
+}
+
+tritd_status tritd_triple_product_f64(const double* A, const double* B, const double* C, int64_t n1,
+                                      int64_t n2, int64_t n3, int32_t r, double* X) {
+    return guarded([&] {
+        check_dims(n1, n2, n3, r);
+        need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
+        pick_device(-1);
+        const int64_t R = (int64_t)r * r;
+        DBuf dA, dB, dC, dX;
+        dA.alloc(n1 * R); dB.alloc(R * n2); dC.alloc(R * n3); dX.alloc((size_t)(n1 * n2 * n3));
+        TRITD_HIP(hipMemcpy(dA.p, A, dA.n * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dB.p, B, dB.n * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dC.p, C, dC.n * 8, hipMemcpyHostToDevice));
+        const tritd_status s = tritd_dev_triple_product_f64(dA.p, dB.p, dC.p, n1, n2, n3, r, dX.p, nullptr);
+        if (s != TRITD_OK) throw Error(s, g_last_error);
+        TRITD_HIP(hipMemcpy(X, dX.p, dX.n * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+tritd_status tritd_dev_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t mode,
+                                  double* Xn, void* stream) {
+    return guarded([&] {
+        if (mode < 1 || mode > 3) throw Error(TRITD_ERR_ARG, "Mode must be 1, 2, or 3.");  // unfold.m:12
+        if (n1 <= 0 || n2 <= 0 || n3 <= 0) throw Error(TRITD_ERR_ARG, "tensor dimensions must be positive");
+        need(X, "X"); need(Xn, "Xn");
+        hipStream_t st = as_stream(stream);
+        if (mode == 1)
+            TRITD_HIP(hipMemcpyAsync(Xn, X, (size_t)(n1 * n2 * n3) * 8, hipMemcpyDeviceToDevice, st));
+        else if (mode == 2)
+            launch_transpose_batched(X, Xn, n1, n2, n3, st);
+        else
+            launch_transpose_batched(X, Xn, n1 * n2, n3, 1, st);
+    });
+}
+
+tritd_status tritd_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t mode,
+                              double* Xn) {
+    return guarded([&] {
+        if (mode < 1 || mode > 3) throw Error(TRITD_ERR_ARG, "Mode must be 1, 2, or 3.");
+        if (n1 <= 0 || n2 <= 0 || n3 <= 0) throw Error(TRITD_ERR_ARG, "tensor dimensions must be positive");
+        need(X, "X"); need(Xn, "Xn");
+        pick_device(-1);
+        const size_t n = (size_t)(n1 * n2 * n3);
+        DBuf a, b;
+        a.alloc(n); b.alloc(n);
+        TRITD_HIP(hipMemcpy(a.p, X, n * 8, hipMemcpyHostToDevice));
+        const tritd_status s = tritd_dev_unfold_f64(a.p, n1, n2, n3, mode, b.p, nullptr);
+        if (s != TRITD_OK) throw Error(s, g_last_error);
+        TRITD_HIP(hipMemcpy(Xn, b.p, n * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+tritd_status tritd_dev_soft_threshold_f64(const double* X, int64_t n, double lam, double* Y,
+                                          void* stream) {
+    return guarded([&] {
+        if (n < 0) throw Error(TRITD_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        need(X, "X"); need(Y, "Y");
+        launch_soft_threshold(X, n, lam, Y, as_stream(stream));
+    });
+}
+
+tritd_status tritd_soft_threshold_f64(const double* X, int64_t n, double lam, double* Y) {
+    return guarded([&] {
+        if (n < 0) throw Error(TRITD_ERR_ARG, "n must be >= 0");
+        if (n == 0) return;
+        need(X, "X"); need(Y, "Y");
+        pick_device(-1);
+        DBuf a, b;
+        a.alloc(n); b.alloc(n);
+        TRITD_HIP(hipMemcpy(a.p, X, n * 8, hipMemcpyHostToDevice));
+        launch_soft_threshold(a.p, n, lam, b.p, nullptr);
+        TRITD_HIP(hipMemcpy(Y, b.p, n * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+tritd_status tritd_build_design_f64(char which, const double* P, const double* Q, int64_t nP,
+                                    int64_t nQ, int32_t r, double* out) {
+    return guarded([&] {
+        if (which != 'F' && which != 'G' && which != 'H') throw Error(TRITD_ERR_ARG, "which must be 'F', 'G' or 'H'");
+        if (nP <= 0 || nQ <= 0 || r <= 0) throw Error(TRITD_ERR_ARG, "sizes must be positive");
+        need(P, "P"); need(Q, "Q"); need(out, "out");
+        pick_device(-1);
+        const int64_t R = (int64_t)r * r;
+        // P: 'F' -> B (r,nP,r); 'G','H' -> A (nP,r,r).  Q: 'F','G' -> C (r,r,nQ); 'H' -> B (r,nQ,r)
+        DBuf dP, dQ, dO;
+        dP.alloc(nP * R); dQ.alloc(nQ * R); dO.alloc(R * nP * nQ);
+        TRITD_HIP(hipMemcpy(dP.p, P, dP.n * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dQ.p, Q, dQ.n * 8, hipMemcpyHostToDevice));
+        launch_design(which, dP.p, dQ.p, nP, nQ, r, dO.p, nullptr);
+        TRITD_HIP(hipMemcpy(out, dO.p, dO.n * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"

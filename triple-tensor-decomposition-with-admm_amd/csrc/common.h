@@ -1,0 +1,96 @@
+// Shared definitions for libtritd (MI355X / gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#include "tritd.h"
+
+namespace tritd {
+
+// Error carried from the point of failure to the C-ABI boundary, where it is
+// turned into a tritd_status + thread-local message (api.cpp).
+struct Error : std::runtime_error {
+    tritd_status code;
+    Error(tritd_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define TRITD_HIP(expr)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            throw ::tritd::Error(e_ == hipErrorOutOfMemory ? TRITD_ERR_NOMEM : TRITD_ERR_HIP, \
+                                 std::string(#expr) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+#define TRITD_CHECK_LAUNCH() TRITD_HIP(hipGetLastError())
+
+__host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int64_t cdiv(int64_t x, int64_t m) { return (x + m - 1) / m; }
+
+// Padded rank R -> RP (multiple of 16, the f64 MFMA tile edge).  The kernels
+// are instantiated for these RP values (r = 1..8).
+inline int padded_rank(int R) { return (int)round_up(R, 16); }
+inline bool rp_supported(int RP) { return RP == 16 || RP == 32 || RP == 48 || RP == 64; }
+
+// Geometry of one shard in the device layout:
+//   big tensors (D, O, E, Y_L, Y_O, T) are TILE-MAJOR ("TM"):
+//     ij-tile g = (j*n1p + i)/16 (16 consecutive rows i of one fibre j),
+//     t-tile tt = t/16; tile (g, tt) = 256 contiguous doubles at (g*ntt + tt)*256.
+//     Inside a tile, element (r, l) of the f64 MFMA C/D fragment
+//     (t%16 = (l>>4) + 4r, i%16 = l&15) sits at (r>>1)*128 + 2l + (r&1), so a
+//     wave reads/writes a tile as two fully contiguous 1 KB dwordx4 sweeps and
+//     walks its ij-tile's t-tiles as one contiguous stream.  Pads are zero.
+//   padded column-major ("PC") X[(t*n2 + j)*n1p + i] is used only at the
+//     host boundary and by the primitives.
+//   factors      Ah[i*RP+k], AhT[k*n1p+i], Bh[j*RP+k], Ch[t*RP+k], ChT[k*n3p+t]
+//   W            Wk[k*plane + j*n1p + i] (plane = n1p*n2)
+struct Geom {
+    int64_t n1 = 0, n2 = 0, n3 = 0;  // global problem
+    int64_t i0 = 0, i1 = 0;          // shard rows
+    int64_t n1l = 0;                 // i1 - i0
+    int64_t n1p = 0, n3p = 0;        // padded
+    int r = 0, R = 0, RP = 0;
+    int64_t plane = 0;               // n1p * n2
+    int64_t Np = 0;                  // plane * n3p
+    int64_t tiles = 0;               // plane / 16 (ij-tiles of 16 rows)
+    int64_t ntt = 0;                 // n3p / 16 (t-tiles)
+};
+
+inline Geom make_geom(int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1, int r) {
+    Geom g;
+    g.n1 = n1; g.n2 = n2; g.n3 = n3; g.i0 = i0; g.i1 = i1; g.n1l = i1 - i0;
+    g.n1p = round_up(g.n1l, 16);
+    g.n3p = round_up(n3, 16);
+    g.r = r; g.R = r * r; g.RP = padded_rank(g.R);
+    g.plane = g.n1p * n2;
+    g.Np = g.plane * g.n3p;
+    g.tiles = g.plane / 16;
+    g.ntt = g.n3p / 16;
+    return g;
+}
+
+// Scalars of one ADMM iteration, precomputed on the host from the
+// deterministic mu schedule (triple_decomp_ADMM.m:16-17,56-57) so that every
+// device expression uses the same IEEE scalars MATLAB would.
+struct IterScalars {
+    double muL, muO;
+    double invL, invO;   // 1/muL, 1/muO          (:41,:42,:46)
+    double thr;          // lambda/muO            (:47)
+    double den;          // muL + muO             (:43)
+    double invL_next;    // 1/muL of the next iteration (fused T formation, :33)
+};
+
+// TM offset of element (i, j, t) of a shard (i < n1p, t < n3p)
+__host__ __device__ inline int64_t tm_offset(int64_t i, int64_t j, int64_t t, int64_t n1p, int64_t ntt) {
+    const int64_t g = (j * n1p + i) >> 4;
+    const int il = (int)(i & 15), tl = (int)(t & 15);
+    const int r = tl >> 2, l = ((tl & 3) << 4) | il;
+    return ((g * ntt + (t >> 4)) << 8) + ((r >> 1) << 7) + (l << 1) + (r & 1);
+}
+
+}  // namespace tritd

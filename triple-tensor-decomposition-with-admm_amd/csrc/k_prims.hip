@@ -1,0 +1,331 @@
+// Primitive kernels: the API-level L1 ops of fast_robust_triple_tensor/ and
+// the reductions the solver needs outside the loop.
+//   K0 unfold          unfold.m:1-13       (LDS-tiled batched transpose)
+//   K6 soft_threshold  soft_threshold.m:2  (16 B/lane streaming)
+//   triple_product     triple_product.m:6  (MFMA, same tile as K5's L)
+//   buildF/G/H         buildF.m:17-21 etc. (design matrices, for parity only)
+#include "kernels.h"
+
+namespace tritd {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------------------
+// sum of squares of a padded tensor (pads are zero) -> per-block partials
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sumsq(const double* __restrict__ X, int64_t n,
+                                               double* partial) {
+    double s = 0.0;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+        s = fma(X[e], X[e], s);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+        partial[2 * blockIdx.x + 1] = 0.0;
+    }
+}
+
+int sumsq_blocks(const Geom& g) {
+    int64_t b = cdiv(g.Np, 256 * 8);
+    return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048);
+}
+
+void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nblocks,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(k_sumsq, dim3(nblocks), dim3(256), 0, st, X, g.Np, partial);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// triple product L(i,j,t) = sum_k Ah(i,k) Bh(j,k) Ch(t,k) in the padded layout.
+// mode 0: write L; mode 1: per-block partials of sum (L-X)^2 and sum X^2
+// (the driver's RRE, traffic_triple_comparison.m:62-63,194-199).
+// ---------------------------------------------------------------------------
+template <int RP, int MODE>
+__global__ __launch_bounds__(512) void k_tp(const double* __restrict__ Ah,
+                                            const double* __restrict__ Bh,
+                                            const double* __restrict__ ChT, double* L,
+                                            const double* __restrict__ X, double* partial,
+                                            int64_t n1p, int64_t n3p, int64_t plane, int64_t tiles) {
+    constexpr int KS = RP / 4;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int il = lane & 15, tg = lane >> 4;
+    const int64_t tile = (int64_t)blockIdx.x * 8 + wid;
+    const bool active = tile < tiles;
+    const int64_t qper = n1p >> 4;
+    const int64_t j = active ? tile / qper : 0;
+    const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
+    const int64_t base = (tile << 4) + il;
+    double kr[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int k = 4 * s + tg;
+        kr[s] = active ? Ah[i * RP + k] * Bh[j * RP + k] : 0.0;
+    }
+    double sn = 0.0, sd = 0.0;
+    if (active) {
+        for (int64_t t0 = 0; t0 < n3p; t0 += 16) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ChT[(int64_t)(4 * s + tg) * n3p + t0 + il],
+                                                           kr[s], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t off = (t0 + tg + 4 * r) * plane + base;
+                if (MODE == 0) {
+                    L[off] = acc[r];
+                } else {
+                    const double x = X[off];
+                    const double dlt = acc[r] - x;
+                    sn += dlt * dlt;
+                    sd += x * x;
+                }
+            }
+        }
+    }
+    if (MODE == 1) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            sn += __shfl_xor(sn, off);
+            sd += __shfl_xor(sd, off);
+        }
+        __shared__ double red[2][8];
+        if (lane == 0) {
+            red[0][wid] = sn;
+            red[1][wid] = sd;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double a = 0.0, b = 0.0;
+            for (int w = 0; w < 8; ++w) {
+                a += red[0][w];
+                b += red[1][w];
+            }
+            partial[2 * blockIdx.x] = a;
+            partial[2 * blockIdx.x + 1] = b;
+        }
+    }
+}
+
+int tp_grid(const Geom& g) { return (int)cdiv(g.tiles, 8); }
+
+void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
+               const double* X, double* partial, int mode, hipStream_t st) {
+    const dim3 grid(tp_grid(g)), block(512);
+#define TP_CASE(RPV)                                                                            \
+    case RPV:                                                                                   \
+        if (mode == 0)                                                                          \
+            hipLaunchKernelGGL((k_tp<RPV, 0>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
+                               g.n1p, g.n3p, g.plane, g.tiles);                                 \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_tp<RPV, 1>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
+                               g.n1p, g.n3p, g.plane, g.tiles);                                 \
+        break;
+    switch (g.RP) {
+        TP_CASE(16)
+        TP_CASE(32)
+        TP_CASE(48)
+        TP_CASE(64)
+        default:
+            throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by triple_product");
+    }
+#undef TP_CASE
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// K0: batched transpose in[b][c][r] (r fastest) -> out[b][r][c] (c fastest).
+//   unfold mode 2 (permute [2 1 3]): rows n1, cols n2, batch n3
+//   unfold mode 3 (permute [3 1 2]): rows n1*n2, cols n3, batch 1
+// 64 x 64 tile through LDS, 16-byte global accesses on both sides.
+// ---------------------------------------------------------------------------
+constexpr int TT = 64;
+__global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in,
+                                                   double* __restrict__ out, int64_t rows,
+                                                   int64_t cols) {
+    __shared__ double tile[TT][TT + 1];
+    const int64_t b = blockIdx.z;
+    const int64_t r0 = (int64_t)blockIdx.x * TT, c0 = (int64_t)blockIdx.y * TT;
+    const double* src = in + b * rows * cols;
+    double* dst = out + b * rows * cols;
+    const int th = threadIdx.x;
+    const bool full = (r0 + TT <= rows) && (c0 + TT <= cols) && ((rows & 1) == 0) && ((cols & 1) == 0);
+    // load: thread -> (c = th/32 + 8m, r = 2*(th%32))
+    {
+        const int rr = 2 * (th & 31), cc = th >> 5;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int c = cc + 8 * m;
+            const int64_t gc = c0 + c, gr = r0 + rr;
+            if (full) {
+                const double2 v = *reinterpret_cast<const double2*>(src + gc * rows + gr);
+                tile[c][rr] = v.x;
+                tile[c][rr + 1] = v.y;
+            } else {
+                tile[c][rr] = (gc < cols && gr < rows) ? src[gc * rows + gr] : 0.0;
+                tile[c][rr + 1] = (gc < cols && gr + 1 < rows) ? src[gc * rows + gr + 1] : 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    // store: thread -> (r = th/32 + 8m, c = 2*(th%32))
+    {
+        const int cc = 2 * (th & 31), rr = th >> 5;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int r = rr + 8 * m;
+            const int64_t gr = r0 + r, gc = c0 + cc;
+            if (full) {
+                *reinterpret_cast<double2*>(dst + gr * cols + gc) = double2{tile[cc][r], tile[cc + 1][r]};
+            } else {
+                if (gr < rows && gc < cols) dst[gr * cols + gc] = tile[cc][r];
+                if (gr < rows && gc + 1 < cols) dst[gr * cols + gc + 1] = tile[cc + 1][r];
+            }
+        }
+    }
+}
+
+void launch_transpose_batched(const double* in, double* out, int64_t rows, int64_t cols,
+                              int64_t batch, hipStream_t st) {
+    if (batch > 65535) throw Error(TRITD_ERR_ARG, "transpose batch too large");
+    const dim3 grid((unsigned)cdiv(rows, TT), (unsigned)cdiv(cols, TT), (unsigned)batch);
+    hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, st, in, out, rows, cols);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// K6: soft_threshold.m:2  Y = sign(X).*max(abs(X)-lam, 0)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double st1(double x, double lam) {
+    const double s = x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x));
+    return s * fmax(fabs(x) - lam, 0.0);
+}
+
+__global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict__ X, int64_t n,
+                                                        double lam, double* __restrict__ Y) {
+    const int64_t n2 = n >> 1;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const d2v* X2 = reinterpret_cast<const d2v*>(X);
+    d2v* Y2 = reinterpret_cast<d2v*>(Y);
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n2; e += stride) {
+        const d2v v = __builtin_nontemporal_load(X2 + e);
+        d2v o;
+        o.x = st1(v.x, lam);
+        o.y = st1(v.y, lam);
+        __builtin_nontemporal_store(o, Y2 + e);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) Y[n - 1] = st1(X[n - 1], lam);
+}
+
+void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hipStream_t st) {
+    if (((uintptr_t)X | (uintptr_t)Y) & 15) throw Error(TRITD_ERR_ARG, "soft_threshold: 16-B alignment");
+    int64_t blocks = cdiv(n / 2, 256 * 4);
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_soft_threshold, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// buildF/G/H: out(k, a + nA*b), k = p + r*q, reference layouts in, column-major out
+//   'F': out(k, j + n2 t) = B(p,j,q) C(p,q,t)      (buildF.m:12)
+//   'G': out(k, i + n1 t) = A(i,p,q) C(p,q,t)      (buildG.m:12)
+//   'H': out(k, i + n1 j) = A(i,p,q) B(p,j,q)      (buildH.m:12)
+// ---------------------------------------------------------------------------
+template <char W>
+__global__ __launch_bounds__(256) void k_design(const double* P, const double* Q, int64_t nP,
+                                                int64_t nQ, int r, double* out) {
+    const int R = r * r;
+    const int64_t total = (int64_t)R * nP * nQ;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * 256) {
+        const int k = (int)(e % R);
+        const int64_t col = e / R;
+        const int64_t a = col % nP, b = col / nP;
+        const int p = k % r, q = k / r;
+        double x, y;
+        if (W == 'F') {  // P = B (r,nP=n2,r), Q = C (r,r,nQ=n3)
+            x = P[p + (int64_t)r * (a + nP * q)];
+            y = Q[k + (int64_t)R * b];
+        } else if (W == 'G') {  // P = A (nP=n1,r,r), Q = C
+            x = P[a + nP * k];
+            y = Q[k + (int64_t)R * b];
+        } else {  // 'H': P = A, Q = B (r,nQ=n2,r)
+            x = P[a + nP * k];
+            y = Q[p + (int64_t)r * (b + nQ * q)];
+        }
+        out[e] = x * y;
+    }
+}
+
+void launch_design(char which, const double* P, const double* Q, int64_t nP, int64_t nQ, int r,
+                   double* out, hipStream_t st) {
+    const int64_t total = (int64_t)r * r * nP * nQ;
+    int64_t blocks = cdiv(total, 256);
+    if (blocks > 16384) blocks = 16384;
+    if (blocks < 1) blocks = 1;
+    const dim3 grid((unsigned)blocks), block(256);
+    if (which == 'F')
+        hipLaunchKernelGGL(k_design<'F'>, grid, block, 0, st, P, Q, nP, nQ, r, out);
+    else if (which == 'G')
+        hipLaunchKernelGGL(k_design<'G'>, grid, block, 0, st, P, Q, nP, nQ, r, out);
+    else
+        hipLaunchKernelGGL(k_design<'H'>, grid, block, 0, st, P, Q, nP, nQ, r, out);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// column-major shard <-> tile-major (common.h).  One-off per solve.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_to_tm(const double* __restrict__ src, int64_t ld,
+                                               int64_t n1l, int64_t n2, int64_t n3, int64_t n1p,
+                                               int64_t ntt, int64_t Np, double* __restrict__ dst) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < Np; e += (int64_t)gridDim.x * 256) {
+        const int64_t tile = e >> 8;
+        const int64_t g = tile / ntt, tt = tile - g * ntt;
+        const int w = (int)(e & 255);
+        const int p = w >> 7, l = (w & 127) >> 1, q = w & 1;
+        const int r = 2 * p + q;
+        const int64_t t = 16 * tt + (l >> 4) + 4 * r;
+        const int64_t row = 16 * g + (l & 15);
+        const int64_t j = row / n1p, i = row - j * n1p;
+        dst[e] = (i < n1l && t < n3) ? src[(t * n2 + j) * ld + i] : 0.0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_from_tm(const double* __restrict__ src, int64_t n1l,
+                                                 int64_t n2, int64_t n3, int64_t n1p, int64_t ntt,
+                                                 double* __restrict__ dst, int64_t ld) {
+    const int64_t total = n1l * n2 * n3;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * 256) {
+        const int64_t i = e % n1l, jt = e / n1l;
+        const int64_t j = jt % n2, t = jt / n2;
+        dst[(t * n2 + j) * ld + i] = src[tm_offset(i, j, t, n1p, ntt)];
+    }
+}
+
+static unsigned grid_for(int64_t n) {
+    int64_t b = cdiv(n, 256);
+    return (unsigned)(b > 16384 ? 16384 : (b < 1 ? 1 : b));
+}
+
+void launch_to_tm(const Geom& g, const double* src, int64_t ld, double* dst, hipStream_t st) {
+    hipLaunchKernelGGL(k_to_tm, dim3(grid_for(g.Np)), dim3(256), 0, st, src, ld, g.n1l, g.n2, g.n3,
+                       g.n1p, g.ntt, g.Np, dst);
+    TRITD_CHECK_LAUNCH();
+}
+
+void launch_from_tm(const Geom& g, const double* src, double* dst, int64_t ld, hipStream_t st) {
+    hipLaunchKernelGGL(k_from_tm, dim3(grid_for(g.n1l * g.n2 * g.n3)), dim3(256), 0, st, src,
+                       g.n1l, g.n2, g.n3, g.n1p, g.ntt, dst, ld);
+    TRITD_CHECK_LAUNCH();
+}
+
+}  // namespace tritd

@@ -1,0 +1,77 @@
+// Kernel launchers (host side) for libtritd.  All launches are asynchronous
+// on the given stream; every ADMM-loop kernel early-exits when *stop != 0 so
+// that iterations enqueued past the stop test of triple_decomp_ADMM.m:63
+// become no-ops without a host round trip.
+#pragma once
+
+#include "common.h"
+
+namespace tritd {
+
+struct DevState;  // solver.cpp
+
+// ---- K5: fused ADMM update (k_admm.hip) ----------------------------------
+struct K5Args {
+    const double* D;
+    double* O;
+    double* E;
+    double* YL;
+    double* YO;
+    double* T;
+    double* Wk;
+    const double* Ah;
+    const double* Bh;
+    const double* Ch;
+    const double* ChT;
+    double* partial;  // [grid][2] sums of resL^2, resO^2
+    int64_t n1p, n2, n3p, plane, tiles, ntt;
+    IterScalars s;
+    const int* stop;
+};
+int k5_grid(const Geom& g);
+void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st);
+// partial sums -> out[0..1] (fixed-order tree)
+void launch_reduce_pairs(const double* partial, int n, double* out, const int* stop, hipStream_t st);
+// errHist bookkeeping + stop test (triple_decomp_ADMM.m:59,63)
+void launch_finish(const double* ss, double normD, int k, double tol, double* errHist, double* errL,
+                   double* errO, int* ctrl, hipStream_t st);
+
+// ---- contractions and small linear algebra (k_contract.hip) ---------------
+void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
+               hipStream_t st);
+void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, const int* stop,
+               hipStream_t st);
+int m3_split(const Geom& g);
+void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
+               double* M3, const int* stop, hipStream_t st);
+// G = X^T X over `rows` rows of a row-major [rows][RP] factor
+void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop, hipStream_t st);
+// Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere)
+void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
+                  int* flags, const int* stop, hipStream_t st);
+// Y = M * Ginv ([rows][RP]); optional transposed copy YT[k*ldT + i]
+void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, double* Y, double* YT,
+                  int64_t ldT, const int* stop, hipStream_t st);
+// out = sum_p in[p] (fixed order), written back to every in[p]  (virtual shards)
+void launch_vsum(double* const* bufs, int nbufs, int64_t count, hipStream_t st);
+
+// ---- primitives (k_prims.hip) ---------------------------------------------
+void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nblocks,
+                         hipStream_t st);
+int sumsq_blocks(const Geom& g);
+// triple product of device factors into the padded layout (mode 0) or the
+// RRE partial sums against X (mode 1: partial[2*b] = sum (L-X)^2, [2*b+1] = sum X^2)
+int tp_grid(const Geom& g);
+void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
+               const double* X, double* partial, int mode, hipStream_t st);
+void launch_transpose_batched(const double* in, double* out, int64_t rows, int64_t cols,
+                              int64_t batch, hipStream_t st);
+// layout conversions of the big tensors: column-major shard (leading dim ld,
+// n1l x n2 x n3) <-> tile-major (common.h)
+void launch_to_tm(const Geom& g, const double* src, int64_t ld, double* dst, hipStream_t st);
+void launch_from_tm(const Geom& g, const double* src, double* dst, int64_t ld, hipStream_t st);
+void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hipStream_t st);
+void launch_design(char which, const double* P, const double* Q, int64_t nP, int64_t nQ, int r,
+                   double* out, hipStream_t st);
+
+}  // namespace tritd

@@ -1,0 +1,406 @@
+// Device-resident ADMM loop of fast_robust_triple_tensor/triple_decomp_ADMM.m:31-66.
+//
+// One iteration = four phases separated by the three all-reduces of the
+// mode-1 sharded schedule:
+//   A  M1, solve A (update_A :73-81), A^TA partial, M2 partial     -> red1
+//   B  solve B (update_B :83-88), B^TB, M3 partial (K2)             -> red2
+//   C  solve C (update_C :90-95), C^TC, fused update K5 (:38-53,:33) -> red3
+//   D  errHist, stop test (:59-65)
+// With one GPU the all-reduces vanish; with RCCL they are ncclAllReduce on
+// the session stream; virtual-shard groups (api.cpp) sum the red buffers of
+// several sessions on one device instead.
+#include "solver.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace tritd {
+
+void emit_line(const char* line);  // api.cpp
+
+// ---------------------------------------------------------------------------
+// layout conversions (reference shapes <-> CP factor matrices)
+// ---------------------------------------------------------------------------
+void pack_A(const Geom& g, const double* A, std::vector<double>& Ah, std::vector<double>& AhT) {
+    Ah.assign(g.n1p * g.RP, 0.0);
+    AhT.assign((size_t)g.RP * g.n1p, 0.0);
+    for (int64_t il = 0; il < g.n1l; ++il)
+        for (int k = 0; k < g.R; ++k) {
+            const double v = A[(g.i0 + il) + g.n1 * k];  // A(i,p,q) at i + n1*(p + r*q)
+            Ah[il * g.RP + k] = v;
+            AhT[(size_t)k * g.n1p + il] = v;
+        }
+}
+
+void pack_B(const Geom& g, const double* B, std::vector<double>& Bh) {
+    Bh.assign(g.n2 * g.RP, 0.0);
+    const int r = g.r;
+    for (int64_t j = 0; j < g.n2; ++j)
+        for (int q = 0; q < r; ++q)
+            for (int p = 0; p < r; ++p) Bh[j * g.RP + p + r * q] = B[p + r * (j + g.n2 * q)];
+}
+
+void pack_C(const Geom& g, const double* C, std::vector<double>& Ch, std::vector<double>& ChT) {
+    Ch.assign(g.n3p * g.RP, 0.0);
+    ChT.assign((size_t)g.RP * g.n3p, 0.0);
+    for (int64_t t = 0; t < g.n3; ++t)
+        for (int k = 0; k < g.R; ++k) {
+            const double v = C[k + (int64_t)g.R * t];  // C(p,q,t) at p + r*q + R*t
+            Ch[t * g.RP + k] = v;
+            ChT[(size_t)k * g.n3p + t] = v;
+        }
+}
+
+void unpack_A(const Geom& g, const std::vector<double>& Ah, double* A) {
+    for (int64_t il = 0; il < g.n1l; ++il)
+        for (int k = 0; k < g.R; ++k) A[(g.i0 + il) + g.n1 * k] = Ah[il * g.RP + k];
+}
+
+void unpack_B(const Geom& g, const std::vector<double>& Bh, double* B) {
+    const int r = g.r;
+    for (int64_t j = 0; j < g.n2; ++j)
+        for (int q = 0; q < r; ++q)
+            for (int p = 0; p < r; ++p) B[p + r * (j + g.n2 * q)] = Bh[j * g.RP + p + r * q];
+}
+
+void unpack_C(const Geom& g, const std::vector<double>& Ch, double* C) {
+    for (int64_t t = 0; t < g.n3; ++t)
+        for (int k = 0; k < g.R; ++k) C[k + (int64_t)g.R * t] = Ch[t * g.RP + k];
+}
+
+// ---------------------------------------------------------------------------
+Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n2, int64_t n3,
+                 int64_t i0, int64_t i1, int r, const tritd_opts& o, const double* A0,
+                 const double* B0, const double* C0, tritd_comm* comm, uint32_t flags,
+                 hipStream_t shared_stream, bool defer_normD)
+    : device_(device), o_(o), comm_(comm) {
+    TRITD_HIP(hipSetDevice(device_));
+    if (shared_stream) {
+        st_ = shared_stream;
+    } else {
+        TRITD_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+        own_stream_ = true;
+    }
+    g_ = make_geom(n1, n2, n3, i0, i1, r);
+    if (!rp_supported(g_.RP)) throw Error(TRITD_ERR_UNSUPPORTED, "r must be in 1..8 for the fp64 path");
+
+    // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
+    mu_.resize((size_t)o_.maxIter + 2);
+    {
+        double mu = o_.mu;
+        const double mu_max = o_.mu * 1e6;
+        for (auto& m : mu_) {
+            m = mu;
+            mu = std::fmin(mu * o_.rho, mu_max);
+        }
+    }
+
+    const size_t Np = (size_t)g_.Np;
+    for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
+        b->alloc(Np);
+        TRITD_HIP(hipMemsetAsync(b->p, 0, Np * sizeof(double), st_));
+    }
+    Wk_.alloc((size_t)g_.RP * g_.plane);
+    TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.n * sizeof(double), st_));
+    Ah_.alloc(g_.n1p * g_.RP);
+    AhT_.alloc((size_t)g_.RP * g_.n1p);
+    Bh_.alloc(g_.n2 * g_.RP);
+    Ch_.alloc(g_.n3p * g_.RP);
+    ChT_.alloc((size_t)g_.RP * g_.n3p);
+    M1_.alloc(g_.n1p * g_.RP);
+    Ginv_.alloc((size_t)g_.RP * g_.RP);
+    BtB_.alloc((size_t)g_.RP * g_.RP);
+    CtC_.alloc((size_t)g_.RP * g_.RP);
+    red1_.alloc(red1_count());
+    red2_.alloc(red2_count());
+    red3_.alloc(2);
+    k5part_.alloc(2 * (size_t)k5_grid(g_));
+    m3part_.alloc((size_t)m3_split(g_) * g_.n3p * g_.RP);
+    sqpart_.alloc(2 * (size_t)sumsq_blocks(g_));
+    const size_t mi = o_.maxIter > 0 ? (size_t)o_.maxIter : 1;
+    errHist_.alloc(mi);
+    errL_.alloc(mi);
+    errO_.alloc(mi);
+    for (DBuf* b : {&errHist_, &errL_, &errO_, &red1_, &red2_, &red3_})
+        TRITD_HIP(hipMemsetAsync(b->p, 0, b->n * sizeof(double), st_));
+    TRITD_HIP(hipMalloc(&ctrl_, 4 * sizeof(int)));
+    TRITD_HIP(hipMemsetAsync(ctrl_, 0, 4 * sizeof(int), st_));
+
+    // D -> tile-major device layout (one-off)
+    if (g_.n1l > 0 && n2 * n3 > 0) {
+        if (flags & TRITD_SESSION_D_ON_DEVICE) {
+            launch_to_tm(g_, D, ldD, D_.p, st_);
+        } else {
+            DBuf tmp;
+            tmp.alloc((size_t)(g_.n1l * n2 * n3));
+            TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * sizeof(double), D, ldD * sizeof(double),
+                                       g_.n1l * sizeof(double), (size_t)(n2 * n3),
+                                       hipMemcpyHostToDevice, st_));
+            launch_to_tm(g_, tmp.p, g_.n1l, D_.p, st_);
+            TRITD_HIP(hipStreamSynchronize(st_));
+        }
+    }
+    upload_factors(A0, B0, C0);
+
+    // normD = norm(D(:))  (:28)
+    const int nb = sumsq_blocks(g_);
+    launch_sumsq_padded(g_, D_.p, sqpart_.p, nb, st_);
+    launch_reduce_pairs(sqpart_.p, nb, red3_.p, nullptr, st_);
+    if (!defer_normD) {
+        allreduce(red3_.p, 2);
+        set_normD_from_red3();
+    }
+
+    // Grams of the initial B, C (replicated factors: no reduction needed)
+    launch_gram(g_.RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    launch_gram(g_.RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+
+    // T of iteration 1 (:33) and W = T x3 C0 for update_A/update_B
+    K5Args a{};
+    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
+    a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
+    a.ntt = g_.ntt;
+    a.s = scalars(1);
+    a.stop = ctrl_;
+    if (o_.maxIter > 0) launch_k5(g_, a, /*prologue=*/true, st_);
+    TRITD_HIP(hipStreamSynchronize(st_));
+}
+
+Session::~Session() {
+    (void)hipSetDevice(device_);
+    if (st_) (void)hipStreamSynchronize(st_);
+    for (auto e : ev_) (void)hipEventDestroy(e);
+    if (ctrl_) (void)hipFree(ctrl_);
+    if (own_stream_ && st_) (void)hipStreamDestroy(st_);
+}
+
+void Session::set_normD_from_red3() {
+    double ss[2];
+    TRITD_HIP(hipMemcpyAsync(ss, red3_.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    normD_ = std::sqrt(ss[0]);
+}
+
+void Session::upload_factors(const double* A0, const double* B0, const double* C0) {
+    std::vector<double> Ah, AhT, Bh, Ch, ChT;
+    pack_A(g_, A0, Ah, AhT);
+    pack_B(g_, B0, Bh);
+    pack_C(g_, C0, Ch, ChT);
+    TRITD_HIP(hipMemcpy(Ah_.p, Ah.data(), Ah.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(AhT_.p, AhT.data(), AhT.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(Bh_.p, Bh.data(), Bh.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(Ch_.p, Ch.data(), Ch.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(ChT_.p, ChT.data(), ChT.size() * sizeof(double), hipMemcpyHostToDevice));
+}
+
+IterScalars Session::scalars(int k) const {
+    IterScalars s;
+    s.muL = mu_[(size_t)k - 1];
+    s.muO = mu_[(size_t)k - 1];
+    s.invL = 1.0 / s.muL;
+    s.invO = 1.0 / s.muO;
+    s.thr = o_.lambda / s.muO;
+    s.den = s.muL + s.muO;
+    s.invL_next = 1.0 / mu_[(size_t)k];
+    return s;
+}
+
+void Session::allreduce(double* buf, int64_t count) {
+    if (!comm_ || !comm_->comm) return;
+    const ncclResult_t r =
+        ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, comm_->comm, st_);
+    if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+int Session::next_iter() {
+    if (k_enq_ >= o_.maxIter) return 0;
+    return ++k_enq_;
+}
+
+void Session::phaseA(int k) {
+    (void)k;
+    const int RP = g_.RP;
+    double* M2 = red1_.p;
+    double* AtA = red1_.p + g_.n2 * RP;
+    launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, Ginv_.p, ctrl_ + 2, ctrl_, st_);
+    launch_apply(RP, M1_.p, g_.n1p, Ginv_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
+}
+
+void Session::phaseB(int k) {
+    (void)k;
+    const int RP = g_.RP;
+    const double* M2 = red1_.p;
+    const double* AtA = red1_.p + g_.n2 * RP;
+    launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, Ginv_.p, ctrl_ + 2, ctrl_, st_);
+    launch_apply(RP, M2, g_.n2, Ginv_.p, Bh_.p, nullptr, 0, ctrl_, st_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+}
+
+void Session::phaseC(int k) {
+    const int RP = g_.RP;
+    const double* AtA = red1_.p + g_.n2 * RP;
+    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :93 ridge
+    launch_apply(RP, red2_.p, g_.n3p, Ginv_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    K5Args a{};
+    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
+    a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
+    a.ntt = g_.ntt;
+    a.s = scalars(k);
+    a.stop = ctrl_;
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
+    launch_k5(g_, a, /*prologue=*/false, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 2], st_));
+    launch_reduce_pairs(k5part_.p, k5_grid(g_), red3_.p, ctrl_, st_);
+}
+
+void Session::phaseD(int k) {
+    launch_finish(red3_.p, normD_, k, o_.tol, errHist_.p, errL_.p, errO_.p, ctrl_, st_);
+}
+
+void Session::maybe_print(int k) {
+    if (!o_.disp || k % 10 != 0) return;
+    if (comm_ && comm_->rank != 0) return;
+    int ctrl[2];
+    double eL, eO;
+    TRITD_HIP(hipMemcpyAsync(ctrl, ctrl_, 2 * sizeof(int), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipMemcpyAsync(&eL, errL_.p + (k - 1), sizeof(double), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipMemcpyAsync(&eO, errO_.p + (k - 1), sizeof(double), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    if (ctrl[1] != k) return;  // stopped earlier: MATLAB never reached iteration k
+    char line[128];
+    std::snprintf(line, sizeof line, "Iter %d, errL=%.2e, errO=%.2e", k, eL, eO);  // :61
+    emit_line(line);
+}
+
+void Session::run(int iters) {
+    TRITD_HIP(hipSetDevice(device_));
+    for (int it = 0; it < iters; ++it) {
+        const int k = next_iter();
+        if (!k) break;
+        if (timing_) {
+            for (int e = 0; e < 6; ++e) {
+                hipEvent_t ev;
+                TRITD_HIP(hipEventCreate(&ev));
+                ev_.push_back(ev);
+            }
+            ev_iter_.push_back(k);
+            TRITD_HIP(hipEventRecord(ev_[ev_.size() - 6], st_));
+        }
+        phaseA(k);
+        allreduce(red1_.p, red1_count());
+        phaseB(k);
+        allreduce(red2_.p, red2_count());
+        phaseC(k);
+        allreduce(red3_.p, 2);
+        phaseD(k);
+        if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 1], st_));
+        maybe_print(k);
+    }
+}
+
+void Session::harvest_timing() {
+    for (size_t b = 0; b + 6 <= ev_.size(); b += 6) {
+        float it = 0, m3 = 0, k5 = 0;
+        TRITD_HIP(hipEventElapsedTime(&it, ev_[b], ev_[b + 5]));
+        TRITD_HIP(hipEventElapsedTime(&m3, ev_[b + 1], ev_[b + 2]));
+        TRITD_HIP(hipEventElapsedTime(&k5, ev_[b + 3], ev_[b + 4]));
+        acc_it_ += it;
+        acc_m3_ += m3;
+        acc_k5_ += k5;
+        ++acc_n_;
+    }
+    for (auto e : ev_) (void)hipEventDestroy(e);
+    ev_.clear();
+    ev_iter_.clear();
+}
+
+void Session::sync(int* done, int* stopped) {
+    TRITD_HIP(hipSetDevice(device_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    if (!ev_.empty()) harvest_timing();
+    int ctrl[3];
+    TRITD_HIP(hipMemcpy(ctrl, ctrl_, 3 * sizeof(int), hipMemcpyDeviceToHost));
+    if (done) *done = ctrl[1];
+    if (stopped) *stopped = ctrl[0];
+}
+
+void Session::set_timing(bool on) {
+    timing_ = on;
+    acc_k5_ = acc_m3_ = acc_it_ = 0;
+    acc_n_ = 0;
+}
+
+void Session::kernel_ms(double* k5, double* m3, double* it, int* samples) {
+    const double n = acc_n_ ? (double)acc_n_ : 1.0;
+    if (k5) *k5 = acc_k5_ / n;
+    if (m3) *m3 = acc_m3_ / n;
+    if (it) *it = acc_it_ / n;
+    if (samples) *samples = acc_n_;
+}
+
+void Session::get(double* A, double* B, double* C, double* O, double* E, int64_t ldOE,
+                  double* errHist, int* iters) {
+    int done = 0, stopped = 0;
+    sync(&done, &stopped);
+    if (A) {
+        std::vector<double> h(Ah_.n);
+        TRITD_HIP(hipMemcpy(h.data(), Ah_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        unpack_A(g_, h, A);
+    }
+    if (B) {
+        std::vector<double> h(Bh_.n);
+        TRITD_HIP(hipMemcpy(h.data(), Bh_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        unpack_B(g_, h, B);
+    }
+    if (C) {
+        std::vector<double> h(Ch_.n);
+        TRITD_HIP(hipMemcpy(h.data(), Ch_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        unpack_C(g_, h, C);
+    }
+    if ((O || E) && g_.n1l > 0) {
+        DBuf tmp;
+        tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));
+        for (auto pr : {std::make_pair(O, &O_), std::make_pair(E, &E_)}) {
+            if (!pr.first) continue;
+            launch_from_tm(g_, pr.second->p, tmp.p, g_.n1l, st_);
+            TRITD_HIP(hipMemcpy2DAsync(pr.first, ldOE * sizeof(double), tmp.p, g_.n1l * sizeof(double),
+                                       g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
+                                       hipMemcpyDeviceToHost, st_));
+            TRITD_HIP(hipStreamSynchronize(st_));
+        }
+    }
+    if (errHist && done > 0)
+        TRITD_HIP(hipMemcpy(errHist, errHist_.p, (size_t)done * sizeof(double), hipMemcpyDeviceToHost));
+    if (iters) *iters = done;
+}
+
+void Session::rre_parts(const double* dX, int64_t ldX, double* num, double* den) {
+    TRITD_HIP(hipSetDevice(device_));
+    DBuf Xp, part, out;
+    Xp.alloc((size_t)g_.Np);
+    TRITD_HIP(hipMemsetAsync(Xp.p, 0, Xp.n * sizeof(double), st_));
+    TRITD_HIP(hipMemcpy2DAsync(Xp.p, g_.n1p * sizeof(double), dX, ldX * sizeof(double),
+                               g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
+                               hipMemcpyDeviceToDevice, st_));
+    const int grid = tp_grid(g_);
+    part.alloc(2 * (size_t)grid);
+    out.alloc(2);
+    launch_tp(g_, Ah_.p, Bh_.p, ChT_.p, nullptr, Xp.p, part.p, 1, st_);
+    launch_reduce_pairs(part.p, grid, out.p, nullptr, st_);
+    double h[2];
+    TRITD_HIP(hipMemcpyAsync(h, out.p, sizeof h, hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    *num = h[0];
+    *den = h[1];
+}
+
+}  // namespace tritd

@@ -1,0 +1,108 @@
+// Device-resident TriTD-ADMM session (one mode-1 shard on one GPU).
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+struct tritd_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = 0;
+};
+
+namespace tritd {
+
+// A device buffer of doubles; freed on destruction.
+struct DBuf {
+    double* p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+    void alloc(size_t count) {
+        n = count;
+        TRITD_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(double)));
+    }
+};
+
+// Host-side layout conversions between the reference shapes and the device
+// factor layout (common.h / DESIGN.md §3).
+void pack_A(const Geom& g, const double* A, std::vector<double>& Ah, std::vector<double>& AhT);
+void pack_B(const Geom& g, const double* B, std::vector<double>& Bh);
+void pack_C(const Geom& g, const double* C, std::vector<double>& Ch, std::vector<double>& ChT);
+void unpack_A(const Geom& g, const std::vector<double>& Ah, double* A);
+void unpack_B(const Geom& g, const std::vector<double>& Bh, double* B);
+void unpack_C(const Geom& g, const std::vector<double>& Ch, double* C);
+
+class Session {
+   public:
+    Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n2, int64_t n3, int64_t i0,
+            int64_t i1, int r, const tritd_opts& o, const double* A0, const double* B0,
+            const double* C0, tritd_comm* comm, uint32_t flags, hipStream_t shared_stream = nullptr,
+            bool defer_normD = false);
+    ~Session();
+
+    // Enqueue iterations (full collective schedule; used without a virtual group)
+    void run(int iters);
+    void sync(int* done, int* stopped);
+    void get(double* A, double* B, double* C, double* O, double* E, int64_t ldOE, double* errHist,
+             int* iters);
+    void rre_parts(const double* dX, int64_t ldX, double* num, double* den);
+    void set_timing(bool on);
+    void kernel_ms(double* k5, double* m3, double* it, int* samples);
+
+    // --- phase interface (virtual shard groups drive these directly) ------
+    // Returns false when iteration k is beyond maxIter (nothing enqueued).
+    int next_iter();  // reserves the next iteration number (or 0)
+    void phaseA(int k);  // M1, solve A, A^TA partial, M2 partial -> red1
+    void phaseB(int k);  // solve B, B^TB, M3 partial -> red2
+    void phaseC(int k);  // solve C, C^TC, K5, norm partial -> red3
+    void phaseD(int k);  // errHist / stop test
+    double* red1() { return red1_.p; }
+    double* red2() { return red2_.p; }
+    double* red3() { return red3_.p; }
+    int64_t red1_count() const { return g_.n2 * g_.RP + (int64_t)g_.RP * g_.RP; }
+    int64_t red2_count() const { return g_.n3p * g_.RP; }
+    hipStream_t stream() const { return st_; }
+    // normD support for groups: local sum of squares in red3[0]
+    void set_normD_from_red3();
+    void maybe_print(int k);
+    const Geom& geom() const { return g_; }
+    int device() const { return device_; }
+
+   private:
+    void allreduce(double* buf, int64_t count);
+    void upload_factors(const double* A0, const double* B0, const double* C0);
+    IterScalars scalars(int k) const;
+
+    int device_;
+    hipStream_t st_ = nullptr;
+    bool own_stream_ = false;
+    Geom g_;
+    tritd_opts o_;
+    tritd_comm* comm_;
+    std::vector<double> mu_;  // mu_[k-1] = muL = muO of iteration k
+    double normD_ = 0.0;
+    int k_enq_ = 0;
+
+    DBuf D_, O_, E_, YL_, YO_, T_, Wk_;
+    DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
+    DBuf red1_, red2_, red3_;
+    DBuf k5part_, m3part_, sqpart_;
+    DBuf errHist_, errL_, errO_;
+    int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag
+
+    bool timing_ = false;
+    std::vector<hipEvent_t> ev_;  // per timed iteration: 6 events
+    std::vector<int> ev_iter_;
+    double acc_k5_ = 0, acc_m3_ = 0, acc_it_ = 0;
+    int acc_n_ = 0;
+    void harvest_timing();
+};
+
+}  // namespace tritd

@@ -1,0 +1,115 @@
+"""ctypes binding of libtritd.so (include/tritd.h).
+
+The library is the product: there is no CPU fallback.  If the shared object
+is missing this module raises at import time; if no gfx950 device is visible
+every compute entry point returns TRITD_ERR_NODEV and the Python wrappers
+raise `TritdError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TRITD_LIB", os.path.join(HERE, "libtritd.so"))
+
+OK = 0
+STATUS_NAMES = {0: "TRITD_OK", 1: "TRITD_ERR_ARG", 2: "TRITD_ERR_OPTS", 3: "TRITD_ERR_HIP",
+                4: "TRITD_ERR_RCCL", 5: "TRITD_ERR_NOMEM", 6: "TRITD_ERR_NODEV",
+                7: "TRITD_ERR_UNSUPPORTED", 8: "TRITD_ERR_STATE"}
+
+OPT_MU, OPT_RHO, OPT_LAMBDA, OPT_LAMBDA2, OPT_MAXITER, OPT_TOL, OPT_DISP = (1 << i for i in range(7))
+OPT_BITS = {"mu": OPT_MU, "rho": OPT_RHO, "lambda": OPT_LAMBDA, "lambda2": OPT_LAMBDA2,
+            "maxIter": OPT_MAXITER, "tol": OPT_TOL, "disp": OPT_DISP}
+SESSION_D_ON_DEVICE = 1
+
+
+class TritdError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class Opts(C.Structure):
+    _fields_ = [("mu", C.c_double), ("rho", C.c_double), ("lambda_", C.c_double),
+                ("lambda2", C.c_double), ("tol", C.c_double), ("maxIter", C.c_int32),
+                ("disp", C.c_int32), ("present", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+PRINT_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
+
+dp = C.POINTER(C.c_double)
+vp = C.c_void_p
+i64 = C.c_int64
+i32 = C.c_int32
+
+# name -> (restype, argtypes); every symbol declared in include/tritd.h
+SIGNATURES = {
+    "tritd_version": (C.c_char_p, []),
+    "tritd_last_error": (C.c_char_p, []),
+    "tritd_set_print_callback": (None, [PRINT_FN, vp]),
+    "tritd_device_count": (C.c_int, [C.POINTER(i32)]),
+    "tritd_admm_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp, vp, vp, vp,
+                                 vp, vp, vp, C.POINTER(i32), i32]),
+    "tritd_session_create": (C.c_int, [C.POINTER(vp), i32, vp, i64, i64, i64, i64, i64, i64, i32,
+                                       C.POINTER(Opts), vp, vp, vp, vp, C.c_uint32]),
+    "tritd_session_run": (C.c_int, [vp, i32]),
+    "tritd_session_sync": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32)]),
+    "tritd_session_get": (C.c_int, [vp, vp, vp, vp, vp, vp, i64, vp, C.POINTER(i32)]),
+    "tritd_session_rre_parts": (C.c_int, [vp, vp, i64, dp, dp]),
+    "tritd_session_set_timing": (C.c_int, [vp, i32]),
+    "tritd_session_kernel_ms": (C.c_int, [vp, dp, dp, dp, C.POINTER(i32)]),
+    "tritd_session_destroy": (None, [vp]),
+    "tritd_comm_unique_id": (C.c_int, [vp]),
+    "tritd_comm_create": (C.c_int, [C.POINTER(vp), vp, i32, i32, i32]),
+    "tritd_comm_destroy": (None, [vp]),
+    "tritd_admm_sharded_virtual_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp,
+                                                 vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32),
+                                                 i32]),
+    "tritd_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp]),
+    "tritd_unfold_f64": (C.c_int, [vp, i64, i64, i64, i32, vp]),
+    "tritd_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp]),
+    "tritd_build_design_f64": (C.c_int, [C.c_char, vp, vp, i64, i64, i32, vp]),
+    "tritd_dev_unfold_f64": (C.c_int, [vp, i64, i64, i64, i32, vp, vp]),
+    "tritd_dev_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp, vp]),
+    "tritd_dev_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp, vp]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libtritd.so not found at {LIB_PATH}: run __graft_entry__.build() "
+                          "(or `make` in triple-tensor-decomposition-with-admm_amd/csrc)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status):
+    if status != OK:
+        raise TritdError(status, lib.tritd_last_error().decode(errors="replace"))
+
+
+def device_count():
+    n = i32(0)
+    check(lib.tritd_device_count(C.byref(n)))
+    return n.value
+
+
+_printer_ref = None
+
+
+def set_printer(fn):
+    """Route opts.disp lines to `fn(str)` (None restores stdout)."""
+    global _printer_ref
+    if fn is None:
+        _printer_ref = PRINT_FN(0)
+    else:
+        _printer_ref = PRINT_FN(lambda line, user: fn(line.decode()))
+    lib.tritd_set_print_callback(_printer_ref, None)

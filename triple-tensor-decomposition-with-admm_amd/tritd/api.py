@@ -1,0 +1,305 @@
+"""Reference-mirroring host API (the MATLAB call surface, in Python).
+
+Every function here keeps the name, argument meaning and failure behaviour of
+the MATLAB file it replaces and runs on the GPU through libtritd.so:
+
+    triple_decomp_ADMM(D, r, opts)          fast_robust_triple_tensor/triple_decomp_ADMM.m:1
+    triple_decomp_ADMM_outlier(D, r, opts)  alias expected at video_triple_comparison.m:54
+    triple_product(A, B, C)                 triple_product.m:1
+    unfold(X, mode)                         unfold.m:1
+    soft_threshold(X, lam)                  soft_threshold.m:1
+    buildF(B, C) / buildG(A, C) / buildH(A, B)   buildF.m:1 / buildG.m:1 / buildH.m:1
+
+Arrays are numpy, MATLAB (column-major) semantics.  `opts` is a dict (or any
+object with attributes) holding the fields the reference reads
+(mu, rho, lambda, lambda2, maxIter, tol, disp); a missing one raises
+``KeyError("Reference to non-existent field 'x'.")`` like MATLAB, extras
+(alphaA, alphaB, origin, ...) are ignored.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import TritdError, check, lib
+
+REQUIRED = ("mu", "rho", "lambda", "lambda2", "maxIter", "tol", "disp")
+
+
+def _get(opts, name):
+    if isinstance(opts, dict):
+        return opts[name] if name in opts else None
+    return getattr(opts, name, None)
+
+
+def make_opts(opts):
+    """dict/struct -> tritd_opts; raises like MATLAB on a missing field."""
+    o = _lib.Opts()
+    present = 0
+    for name in REQUIRED:
+        v = _get(opts, name)
+        if v is None:
+            raise KeyError(f"Reference to non-existent field '{name}'.")
+        present |= _lib.OPT_BITS[name]
+    o.mu = float(_get(opts, "mu"))
+    o.rho = float(_get(opts, "rho"))
+    o.lambda_ = float(_get(opts, "lambda"))
+    o.lambda2 = float(_get(opts, "lambda2"))
+    o.tol = float(_get(opts, "tol"))
+    o.maxIter = int(_get(opts, "maxIter"))
+    o.disp = int(bool(_get(opts, "disp")))
+    o.present = present
+    return o
+
+
+def _f64(X):
+    return np.asarray(X, dtype=np.float64)
+
+
+def _fortran(X):
+    return np.asfortranarray(_f64(X))
+
+
+def _size3(X):
+    if X.ndim > 3:
+        raise ValueError("D must have at most 3 dimensions")
+    s = tuple(X.shape) + (1, 1, 1)
+    return int(s[0]), int(s[1]), int(s[2])
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def initial_factors(n1, n2, n3, r, opts=None, rng=None):
+    """A0, B0, C0 in the order of triple_decomp_ADMM.m:23.  Explicit
+    opts['A0'/'B0'/'C0'] win (MATLAB's Ziggurat randn is not reproducible
+    outside MATLAB, so callers that need parity pass them in)."""
+    A0 = _get(opts, "A0") if opts is not None else None
+    B0 = _get(opts, "B0") if opts is not None else None
+    C0 = _get(opts, "C0") if opts is not None else None
+    rng = rng if rng is not None else np.random.default_rng()
+    if A0 is None:
+        A0 = rng.standard_normal((n1, r, r))
+    if B0 is None:
+        B0 = rng.standard_normal((r, n2, r))
+    if C0 is None:
+        C0 = rng.standard_normal((r, r, n3))
+    A0 = _fortran(A0).reshape((n1, r, r), order="F")
+    B0 = _fortran(B0).reshape((r, n2, r), order="F")
+    C0 = _fortran(C0).reshape((r, r, n3), order="F")
+    return A0, B0, C0
+
+
+def triple_decomp_ADMM(D, r, opts, A0=None, B0=None, C0=None, *, device=-1, return_E=False,
+                       return_iters=False, virtual_shards=0):
+    """[A,B,C,O,errHist] = triple_decomp_ADMM(D, r, opts) on the GPU.
+
+    Extra outputs beyond the reference signature: E (``return_E``) and the
+    iteration count (``return_iters``).  ``virtual_shards=P`` runs the mode-1
+    sharded schedule as P shards on one device (rehearsal of the multi-GPU
+    path)."""
+    o = make_opts(opts)
+    D = _fortran(D)
+    n1, n2, n3 = _size3(D)
+    r = int(r)
+    if A0 is None or B0 is None or C0 is None:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, opts)
+    else:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, dict(A0=A0, B0=B0, C0=C0))
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cf = np.zeros((r, r, n3), order="F")
+    O = np.zeros((n1, n2, n3), order="F")
+    E = np.zeros((n1, n2, n3), order="F")
+    errHist = np.zeros(max(o.maxIter, 1))
+    k = _lib.i32(0)
+    if virtual_shards and virtual_shards > 1:
+        check(lib.tritd_admm_sharded_virtual_f64(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0),
+                                                 _ptr(B0), _ptr(C0), int(virtual_shards), _ptr(A),
+                                                 _ptr(B), _ptr(Cf), _ptr(O), _ptr(E),
+                                                 _ptr(errHist), C.byref(k), int(device)))
+    else:
+        check(lib.tritd_admm_f64(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+                                 _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), _ptr(errHist),
+                                 C.byref(k), int(device)))
+    errHist = errHist[: k.value].copy()  # :68 errHist = errHist(1:k)
+    out = [A, B, Cf, O, errHist]
+    if return_E:
+        out.append(E)
+    if return_iters:
+        out.append(k.value)
+    return tuple(out)
+
+
+# the name video_triple_comparison.m:54 calls (unresolvable in the reference)
+triple_decomp_ADMM_outlier = triple_decomp_ADMM
+
+
+def triple_product(A, B, C_):
+    """Xhat = triple_product(A, B, C)  (triple_product.m:1-7)."""
+    A = _fortran(A)
+    B = _fortran(B)
+    C_ = _fortran(C_)
+    n1, r, _ = _size3(A)
+    n2 = _size3(B)[1]
+    n3 = _size3(C_)[2]
+    X = np.zeros((n1, n2, n3), order="F")
+    check(lib.tritd_triple_product_f64(_ptr(A), _ptr(B), _ptr(C_), n1, n2, n3, r, _ptr(X)))
+    return X
+
+
+def unfold(X, mode):
+    """Xn = unfold(X, mode)  (unfold.m:1-13)."""
+    X = _fortran(X)
+    n1, n2, n3 = _size3(X)
+    shapes = {1: (n1, n2 * n3), 2: (n2, n1 * n3), 3: (n3, n1 * n2)}
+    out = np.zeros(shapes.get(int(mode), (1,)), order="F")
+    check(lib.tritd_unfold_f64(_ptr(X), n1, n2, n3, int(mode), _ptr(out)))
+    return out
+
+
+def soft_threshold(X, lam):
+    """O = soft_threshold(X, lam)  (soft_threshold.m:1-2)."""
+    X = _fortran(X)
+    Y = np.zeros_like(X, order="F")
+    check(lib.tritd_soft_threshold_f64(_ptr(X), X.size, float(lam), _ptr(Y)))
+    return Y
+
+
+def _design(which, P, Q, nP, nQ, r):
+    out = np.zeros((r * r, nP * nQ), order="F")
+    check(lib.tritd_build_design_f64(which.encode(), _ptr(P), _ptr(Q), nP, nQ, r, _ptr(out)))
+    return out
+
+
+def buildF(B, C_):
+    """F = buildF(B, C)  (buildF.m:1-22)."""
+    B = _fortran(B)
+    C_ = _fortran(C_)
+    r, n2, _ = _size3(B)
+    return _design("F", B, C_, n2, _size3(C_)[2], r)
+
+
+def buildG(A, C_):
+    """G = buildG(A, C)  (buildG.m:1-22)."""
+    A = _fortran(A)
+    C_ = _fortran(C_)
+    n1, r, _ = _size3(A)
+    return _design("G", A, C_, n1, _size3(C_)[2], r)
+
+
+def buildH(A, B):
+    """H = buildH(A, B)  (buildH.m:1-22)."""
+    A = _fortran(A)
+    B = _fortran(B)
+    n1, r, _ = _size3(A)
+    return _design("H", A, B, n1, _size3(B)[1], r)
+
+
+# ---------------------------------------------------------------------------
+# Sessions: device-resident loop (bench, multi-GPU)
+# ---------------------------------------------------------------------------
+class Session:
+    """One mode-1 shard [i0, i1) of an n1 x n2 x n3 problem on one GPU.
+
+    D is either a host numpy array holding the shard (column-major, leading
+    dimension ldD) or, with ``d_device_ptr``, a device pointer."""
+
+    def __init__(self, r, opts, A0, B0, C0, *, n1, n2, n3, i0=0, i1=None, D=None,
+                 d_device_ptr=None, ldD=None, device=0, comm=None):
+        self._s = C.c_void_p()
+        o = make_opts(opts)
+        i1 = n1 if i1 is None else i1
+        A0 = _fortran(A0)
+        B0 = _fortran(B0)
+        C0 = _fortran(C0)
+        flags = 0
+        if d_device_ptr is not None:
+            dptr = C.c_void_p(int(d_device_ptr))
+            flags |= _lib.SESSION_D_ON_DEVICE
+            ldD = ldD if ldD is not None else (i1 - i0)
+        else:
+            D = _fortran(D)
+            dptr = _ptr(D)
+            ldD = ldD if ldD is not None else D.shape[0]
+        self.n1, self.n2, self.n3, self.i0, self.i1, self.r = n1, n2, n3, i0, i1, r
+        self.maxIter = o.maxIter
+        check(lib.tritd_session_create(C.byref(self._s), int(device), dptr, int(ldD), n1, n2, n3,
+                                       i0, i1, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+                                       comm.handle if comm is not None else None, flags))
+
+    def run(self, iters):
+        check(lib.tritd_session_run(self._s, int(iters)))
+
+    def sync(self):
+        d, s = _lib.i32(0), _lib.i32(0)
+        check(lib.tritd_session_sync(self._s, C.byref(d), C.byref(s)))
+        return d.value, bool(s.value)
+
+    def get(self):
+        r, n1, n2, n3 = self.r, self.n1, self.n2, self.n3
+        nl = self.i1 - self.i0
+        A = np.zeros((n1, r, r), order="F")
+        B = np.zeros((r, n2, r), order="F")
+        Cf = np.zeros((r, r, n3), order="F")
+        O = np.zeros((nl, n2, n3), order="F")
+        E = np.zeros((nl, n2, n3), order="F")
+        eh = np.zeros(max(self.maxIter, 1))
+        k = _lib.i32(0)
+        check(lib.tritd_session_get(self._s, _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), nl,
+                                    _ptr(eh), C.byref(k)))
+        return dict(A=A, B=B, C=Cf, O=O, E=E, errHist=eh[: k.value].copy(), k=k.value)
+
+    def rre_parts(self, dX_ptr, ldX):
+        num, den = C.c_double(0), C.c_double(0)
+        check(lib.tritd_session_rre_parts(self._s, C.c_void_p(int(dX_ptr)), int(ldX),
+                                          C.byref(num), C.byref(den)))
+        return num.value, den.value
+
+    def set_timing(self, on=True):
+        check(lib.tritd_session_set_timing(self._s, int(bool(on))))
+
+    def kernel_ms(self):
+        a, b, c = C.c_double(0), C.c_double(0), C.c_double(0)
+        n = _lib.i32(0)
+        check(lib.tritd_session_kernel_ms(self._s, C.byref(a), C.byref(b), C.byref(c), C.byref(n)))
+        return dict(fused_update=a.value, mode3=b.value, iteration=c.value, samples=n.value)
+
+    def close(self):
+        if self._s:
+            lib.tritd_session_destroy(self._s)
+            self._s = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Comm:
+    """RCCL communicator owned by libtritd (one process per GPU)."""
+
+    def __init__(self, unique_id: bytes, nranks, rank, device):
+        self.handle = C.c_void_p()
+        buf = C.create_string_buffer(bytes(unique_id), 128)
+        check(lib.tritd_comm_create(C.byref(self.handle), buf, int(nranks), int(rank), int(device)))
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib.tritd_comm_unique_id(buf))
+        return buf.raw
+
+    def close(self):
+        if self.handle:
+            lib.tritd_comm_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+
+__all__ = ["triple_decomp_ADMM", "triple_decomp_ADMM_outlier", "triple_product", "unfold",
+           "soft_threshold", "buildF", "buildG", "buildH", "Session", "Comm", "TritdError",
+           "make_opts", "initial_factors"]

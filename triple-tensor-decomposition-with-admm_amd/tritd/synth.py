@@ -1,0 +1,110 @@
+"""Synthetic workloads for the TriTD-ADMM hot path.
+
+The reference's datasets (`sensor.mat`, CDnet2014 videos) are not shipped
+(SURVEY.md §2 #17), so benchmarks and parity tests run on seeded synthetic
+tensors of the reference shapes.  Everything here is plain numpy data
+generation in MATLAB (column-major) layout: it produces *inputs*, it is not
+part of the accelerated path.
+
+Recipe (SURVEY.md §8d "Synthetic generator"):
+  A*, B*, C* ~ N(0,1) in the reference shapes (n1,r,r), (r,n2,r), (r,r,n3)
+  L* = triple_product(A*, B*, C*)      (triple_product.m:6)
+  S* : Bernoulli(p_out) support, values U(-10 sigma, 10 sigma), sigma = std(L*)
+  D  = L* + S*
+  A0, B0, C0 ~ N(0,1) (seed 123) — the initial factors the MATLAB wrapper would
+  draw with randn (triple_decomp_ADMM.m:23).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# opts of the completion driver (traffic_triple_comparison.m:42-50)
+TRAFFIC_OPTS = dict(maxIter=100, tol=1e-5, mu=1e-3, **{"lambda": 1.8}, lambda2=1e-3, rho=1.25, disp=0)
+# opts of the video driver (video_triple_comparison.m:41-50)
+VIDEO_OPTS = dict(maxIter=100, tol=1e-5, mu=1e-2, **{"lambda": 1.8}, lambda2=1e-2, rho=1.2, disp=0)
+
+
+def hat_factors(A, B, C):
+    """Reference factors -> CP factor matrices:
+    Ahat(i,k)=A(i,p,q), Bhat(j,k)=B(p,j,q), Chat(t,k)=C(p,q,t), k=p+(q-1)r."""
+    n1, r, _ = A.shape
+    n2 = B.shape[1]
+    n3 = C.shape[2]
+    Ah = A.reshape((n1, r * r), order="F")
+    Bh = np.transpose(B, (1, 0, 2)).reshape((n2, r * r), order="F")
+    Ch = C.reshape((r * r, n3), order="F").T
+    return Ah, Bh, Ch
+
+
+def cp_full(Ah, Bh, Ch):
+    """L(i,j,t) = sum_k Ah(i,k) Bh(j,k) Ch(t,k), column-major (n1,n2,n3)."""
+    n1, R = Ah.shape
+    n2 = Bh.shape[0]
+    n3 = Ch.shape[0]
+    # (n1 x R) @ (R x n2*n3) with KR(k, j + n2 t) = Bh(j,k) Ch(t,k)
+    KR = (Bh[:, None, :] * Ch[None, :, :]).reshape((n2 * n3, R), order="F")
+    return (Ah @ KR.T).reshape((n1, n2, n3), order="F")
+
+
+def random_factors(n1, n2, n3, r, seed):
+    rng = np.random.default_rng(seed)
+    A = np.asfortranarray(rng.standard_normal((n1, r, r)))
+    B = np.asfortranarray(rng.standard_normal((r, n2, r)))
+    C = np.asfortranarray(rng.standard_normal((r, r, n3)))
+    return A, B, C
+
+
+def low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123):
+    """Config 1/4/5 generator.  Returns dict(D, Lstar, A0, B0, C0)."""
+    rng = np.random.default_rng(seed)
+    As = np.asfortranarray(rng.standard_normal((n1, r, r)))
+    Bs = np.asfortranarray(rng.standard_normal((r, n2, r)))
+    Cs = np.asfortranarray(rng.standard_normal((r, r, n3)))
+    Lstar = cp_full(*hat_factors(As, Bs, Cs))
+    sigma = float(Lstar.std())
+    support = rng.random((n1, n2, n3)) < p_out
+    vals = rng.uniform(-10.0 * sigma, 10.0 * sigma, size=(n1, n2, n3))
+    D = np.asfortranarray(Lstar + np.where(support, vals, 0.0))
+    A0, B0, C0 = random_factors(n1, n2, n3, r, init_seed)
+    return dict(D=D, Lstar=Lstar, A0=A0, B0=B0, C0=C0)
+
+
+def sensor_like(n1=54, n2=4, n3=1152, r=5, missing=0.10, seed=0, init_seed=123):
+    """Config 2 stand-in: smooth daily-periodic readings + noise, a seeded
+    fraction zeroed (traffic_triple_comparison.m:27-35 zeroes missing entries)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n3)
+    base = rng.uniform(15.0, 25.0, size=(n1, n2, 1))
+    amp = rng.uniform(1.0, 5.0, size=(n1, n2, 1))
+    phase = rng.uniform(0, 2 * np.pi, size=(n1, n2, 1))
+    X = base + amp * np.sin(2 * np.pi * t[None, None, :] / 144.0 + phase)
+    X = X + 0.1 * rng.standard_normal((n1, n2, n3))
+    X = np.asfortranarray(X)
+    mask = rng.random((n1, n2, n3)) < missing
+    Y = X.copy(order="F")
+    Y[mask] = 0.0
+    A0, B0, C0 = random_factors(n1, n2, n3, r, init_seed)
+    return dict(D=Y, X=X, mask=mask, A0=A0, B0=B0, C0=C0)
+
+
+def video_like(n1=240, n2=320, n3=300, r=5, seed=0, init_seed=123):
+    """Config 3 stand-in: static background (rank-1 in time) + moving bright
+    blobs + N(0,2) noise, clipped to 0..255 (video_triple_comparison.m:20-21
+    loads uint8 frames as double)."""
+    rng = np.random.default_rng(seed)
+    bg = rng.uniform(40.0, 200.0, size=(n1, n2))
+    X = np.repeat(bg[:, :, None], n3, axis=2)
+    ii, jj = np.meshgrid(np.arange(n1), np.arange(n2), indexing="ij")
+    for b in range(3):
+        ci0, cj0 = rng.uniform(0, n1), rng.uniform(0, n2)
+        vi, vj = rng.uniform(-1.0, 1.0), rng.uniform(0.5, 2.0)
+        rad = max(2.0, min(n1, n2) / 12.0)
+        for t in range(n3):
+            ci = (ci0 + vi * t) % n1
+            cj = (cj0 + vj * t) % n2
+            blob = (ii - ci) ** 2 + (jj - cj) ** 2 < rad ** 2
+            X[:, :, t][blob] = 250.0
+    X = X + 2.0 * rng.standard_normal(X.shape)
+    X = np.asfortranarray(np.clip(X, 0.0, 255.0))
+    A0, B0, C0 = random_factors(n1, n2, n3, r, init_seed)
+    return dict(D=X.copy(order="F"), X=X, A0=A0, B0=B0, C0=C0)
