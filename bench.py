@@ -1,0 +1,218 @@
+"""TriTD-ADMM benchmark: ADMM iterations/s + final RRE on the synthetic
+512x512x512 r=8 fp64 workload (BASELINE.json configs[3]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A "step" is one ADMM iteration (triple_decomp_ADMM.m:31-66) over the whole
+tensor, device-resident.  With N > 1 ranks the tensor is sharded along
+mode 1 and the three per-iteration all-reduces run over
+RCCL (strong scaling: the problem size is fixed).  Rank 0 prints one JSON
+line.  The CPU baseline is the C restatement of the MATLAB reference
+(oracle/tritd_ref.c, kind "port") timed on a bounded sample on rank 0.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+N_DEFAULT = 512
+R_DEFAULT = 8
+
+
+def ensure_built():
+    if not os.path.exists(os.path.join(PKG, "tritd", "libtritd.so")):
+        subprocess.run(["make", "-j8", "-C", os.path.join(PKG, "csrc")], check=True)
+
+
+def cpu_baseline(D, r, opts, A0, B0, C0, iters):
+    """Time the C restatement of the reference on the host (bounded sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        if not os.path.exists(os.path.join(ROOT, "oracle", "build", "libtritd_ref.so")):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                           stdout=subprocess.DEVNULL)
+        import tritd_ref
+        lib = tritd_ref.load()
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        lib.tritd_ref_set_threads(threads)
+        t0 = time.perf_counter()
+        out = tritd_ref.admm(lib, D, r, opts, A0, B0, C0, max_iters=iters)
+        dt = time.perf_counter() - t0
+        k = out[6]
+        return {"value": k / dt, "unit": "iters/s", "cores": threads, "kind": "port",
+                "sample": "%d ADMM iterations of the same %dx%dx%d r=%d fp64 workload "
+                          "(C restatement of triple_decomp_ADMM.m with its materialised "
+                          "permutes/design matrices, GEMM and pinv; OpenMP; includes per-call "
+                          "setup)" % (k, *D.shape, r),
+                "seconds": dt}
+    except Exception as e:  # the baseline is reported, never the product
+        return {"value": None, "unit": "iters/s", "cores": 0, "kind": "port",
+                "sample": "unavailable: %s" % e}
+
+
+def pmc_traffic():
+    """HBM bytes per fused-update launch from the committed rocprofv3 PMC pass
+    (tools/pmc_traffic.py -> profiles/*_k5_traffic.json), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*k5_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=N_DEFAULT)
+    ap.add_argument("--r", type=int, default=R_DEFAULT)
+    ap.add_argument("--cpu-iters", type=int, default=12)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit("--gpus must match WORLD_SIZE")
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ensure_built()
+    import tritd
+    from tritd import synth
+
+    n, r = args.n, args.r
+    K, W = args.steps, args.warmup
+    maxIter = max(100, K + W)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=maxIter, tol=synth.TRAFFIC_OPTS["tol"])
+    data = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
+    D, Lstar = data["D"], data["Lstar"]
+
+    # mode-1 shard of this rank
+    chunk = (n + world - 1) // world
+    i0, i1 = rank * chunk, min(n, (rank + 1) * chunk)
+    comm = None
+    if world > 1:
+        uid = [tritd.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = tritd.Comm(uid[0], world, rank, local_rank)
+
+    # inputs resident in HBM before the timed region
+    dev = torch.device("cuda", local_rank)
+    D_shard = torch.from_numpy(np.ascontiguousarray(D[i0:i1].transpose(2, 1, 0))).to(dev)
+    sess = tritd.Session(r, opts, data["A0"], data["B0"], data["C0"], n1=n, n2=n, n3=n, i0=i0,
+                         i1=i1, d_device_ptr=D_shard.data_ptr(), ldD=i1 - i0, device=local_rank,
+                         comm=comm)
+    del D_shard
+
+    sess.run(W)
+    sess.sync()
+    sess.set_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.run(K)
+    done, stopped = sess.sync()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    km = sess.kernel_ms()
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if done != W + K or stopped:
+        raise SystemExit("stop test fired inside the timed region (k=%d): timing invalid" % done)
+
+    # finish the solve (untimed) and report the driver RRE at the final k
+    sess.run(maxIter - done)
+    k_final, _ = sess.sync()
+    L_shard = torch.from_numpy(np.ascontiguousarray(Lstar[i0:i1].transpose(2, 1, 0))).to(dev)
+    num, den = sess.rre_parts(L_shard.data_ptr(), i1 - i0)
+    if dist is not None:
+        t = torch.tensor([num, den], device=dev, dtype=torch.float64)
+        dist.all_reduce(t)
+        num, den = float(t[0]), float(t[1])
+    rre = float(np.sqrt(num / den))
+    res = sess.get()
+    errhist_final = float(res["errHist"][-1]) if len(res["errHist"]) else None
+
+    # algorithmic bytes of the dominant kernel (fused update K5), per launch,
+    # on this rank's shard: reads D,Y_L,E,Y_O + writes O,E,Y_L,Y_O,T (9 N-streams)
+    # + W (R * n1 * n2 doubles); SURVEY.md §8d / DESIGN.md §4
+    nl = i1 - i0
+    N_local = nl * n * n
+    k5_bytes = (9 * N_local + r * r * nl * n) * 8
+    k5_ms = km["fused_update"]
+    achieved = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
+    traffic, traffic_src = pmc_traffic()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], args.cpu_iters)
+
+    if rank == 0:
+        line = {
+            "metric": "ADMM iters/sec + final RRE, 512^3 r=8 tensor at 1/2/4/8 MI355X",
+            "value": K / dt,
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": dt * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "synthetic %dx%dx%d fp64 r=%d low-rank + 5%% outliers "
+                                   "(SURVEY.md 8d), traffic opts (traffic_triple_comparison.m:42-50)"
+                                   % (n, n, n, r),
+                       "n1": n, "n2": n, "n3": n, "r": r, "maxIter": maxIter,
+                       "parallelism": "mode1-shard x%d" % world},
+            "rre_final": rre,
+            "k_final": k_final,
+            "errHist_final": errhist_final,
+            "kernel_ms": {"fused_update": k5_ms, "mode3_mttkrp": km["mode3"],
+                          "iteration_events": km["iteration"], "samples": km["samples"]},
+            "roofline": {"kernel": "k5_fused (fused ADMM update + L + W)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": k5_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+    sess.close()
+    if comm is not None:
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
