@@ -112,13 +112,9 @@ def main():
     D, Lstar = data["D"], data["Lstar"]
 
     # mode-1 shard of this rank
-    chunk = (n + world - 1) // world
-    i0, i1 = rank * chunk, min(n, (rank + 1) * chunk)
-    comm = None
-    if world > 1:
-        uid = [tritd.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = tritd.Comm(uid[0], world, rank, local_rank)
+    from tritd.dist import make_comm, shard_bounds
+    i0, i1 = shard_bounds(n, world, rank)
+    comm = make_comm(dist, rank, world, local_rank) if world > 1 else None
 
     # inputs resident in HBM before the timed region
     dev = torch.device("cuda", local_rank)

@@ -1,0 +1,98 @@
+"""Mode-1 sharded restatement of the ADMM loop — TEST INFRASTRUCTURE ONLY.
+
+This is the algebra libtritd runs across GPUs,
+written in numpy with an injected `allreduce(np.ndarray) -> np.ndarray` so
+the CPU tests can drive it with torch.distributed/gloo at world_size 2 and
+compare against the unsharded line-by-line oracle (tritd_oracle.py).
+
+Per iteration k on the shard rows [i0, i1):
+  A  M1 = sum_j W(i,j,:) o B^(j,:)             (W = T x3 C^ from the previous pass)
+     A^ = M1 inv((B^TB) o (C^TC) + l2 I)        update_A, triple_decomp_ADMM.m:73-81
+     red1 = [ M2 = sum_i W(i,:,:) o A^(i,:) | A^TA ]           -> all-reduce
+  B  B^ = M2 inv((A^TA) o (C^TC) + l2 I)        update_B, :83-88
+     red2 = M3 = sum_ij T(i,j,:) A^(i,:) o B^(j,:)             -> all-reduce
+  C  C^ = M3 inv((A^TA) o (B^TB) + 1e-9 I)      update_C, :90-95
+     L, O, E, Y_L, Y_O (:38-53), T_next (:33), W_next = T_next x3 C^
+     red3 = [sum resL^2, sum resO^2]                           -> all-reduce
+  D  errHist / stop test (:59-65)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _hat(A0, B0, C0, r):
+    n1 = A0.shape[0]
+    n2 = B0.shape[1]
+    n3 = C0.shape[2]
+    R = r * r
+    Ah = A0.reshape((n1, R), order="F").copy()
+    Bh = np.transpose(B0, (1, 0, 2)).reshape((n2, R), order="F").copy()
+    Ch = C0.reshape((R, n3), order="F").T.copy()
+    return Ah, Bh, Ch
+
+
+def sharded_admm(D_local, i0, i1, r, opts, A0, B0, C0, allreduce):
+    """Run the sharded schedule on rows [i0, i1).  Returns dict with the local
+    A rows, replicated B, C (reference layouts), local O, E and errHist."""
+    D = np.asarray(D_local, dtype=np.float64)
+    nl, n2, n3 = D.shape
+    n1 = A0.shape[0]
+    R = r * r
+    Ah_full, Bh, Ch = _hat(A0, B0, C0, r)
+    Ah = Ah_full[i0:i1].copy()
+    mu0, rho = float(opts["mu"]), float(opts["rho"])
+    lam, l2 = float(opts["lambda"]), float(opts["lambda2"])
+    maxIter, tol = int(opts["maxIter"]), float(opts["tol"])
+    mus = []
+    mu = mu0
+    for _ in range(maxIter + 1):
+        mus.append(mu)
+        mu = min(mu * rho, mu0 * 1e6)
+
+    O = np.zeros_like(D)
+    E = np.zeros_like(D)
+    YL = np.zeros_like(D)
+    YO = np.zeros_like(D)
+    normD = float(np.sqrt(allreduce(np.array([np.sum(D * D)]))[0]))
+    T = (D - O) + (1.0 / mus[0]) * YL
+    W = np.einsum("ijt,tk->ijk", T, Ch)
+    BtB, CtC = Bh.T @ Bh, Ch.T @ Ch
+    errHist = []
+    k = 0
+    for k in range(1, maxIter + 1):
+        M1 = np.einsum("ijk,jk->ik", W, Bh)
+        Ah = M1 @ np.linalg.inv(BtB * CtC + l2 * np.eye(R))
+        red1 = allreduce(np.concatenate([np.einsum("ijk,ik->jk", W, Ah).ravel(),
+                                         (Ah.T @ Ah).ravel()]))
+        M2, AtA = red1[: n2 * R].reshape(n2, R), red1[n2 * R:].reshape(R, R)
+        Bh = M2 @ np.linalg.inv(AtA * CtC + l2 * np.eye(R))
+        BtB = Bh.T @ Bh
+        M3 = allreduce(np.einsum("ijt,ik,jk->tk", T, Ah, Bh))
+        Ch = M3 @ np.linalg.inv(AtA * BtB + 1e-9 * np.eye(R))
+        CtC = Ch.T @ Ch
+
+        muL = muO = mus[k - 1]
+        L = np.einsum("ik,jk,tk->ijt", Ah, Bh, Ch)
+        R1 = (D - L) + (1.0 / muL) * YL
+        R2 = E - (1.0 / muO) * YO
+        O = (muL * R1 + muO * R2) / (muL + muO)
+        R3 = O + (1.0 / muO) * YO
+        E = np.sign(R3) * np.fmax(np.abs(R3) - lam / muO, 0.0)
+        resL = (D - L) - O
+        resO = O - E
+        YL = YL + muL * resL
+        YO = YO + muO * resO
+        T = (D - O) + (1.0 / mus[k]) * YL
+        W = np.einsum("ijt,tk->ijk", T, Ch)
+        ss = allreduce(np.array([np.sum(resL * resL), np.sum(resO * resO)]))
+        errHist.append(np.sqrt(ss[0]) / normD + np.sqrt(ss[1]) / normD)
+        if k > 1 and abs(errHist[-1] - errHist[-2]) < tol * errHist[-2]:
+            break
+
+    A = np.zeros((n1, r, r), order="F")
+    A.reshape((n1, R), order="F")[i0:i1] = Ah  # rows of this shard only
+    A_loc = Ah.reshape((nl, r, r), order="F")
+    B = np.transpose(Bh.reshape((n2, r, r), order="F"), (1, 0, 2)).copy(order="F")
+    C = Ch.T.reshape((r, r, n3), order="F").copy(order="F")
+    return dict(A_rows=A_loc, B=B, C=C, O=O, E=E, errHist=np.array(errHist), k=k)

@@ -1,0 +1,115 @@
+"""The C-ABI boundary on a host without a GPU: libtritd.so loads, exports
+every entry point include/tritd.h declares, validates arguments the way the
+reference fails, and refuses to compute without a gfx950 device (there is
+no CPU fallback in the product path)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "tritd.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tritd_[a-z0-9_]+)\s*\(", src)) - {"tritd_print_fn"})
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from tritd import _lib
+    return _lib
+
+
+def test_header_and_binding_agree(lib):
+    assert set(declared_symbols()) == set(lib.SIGNATURES)
+
+
+def test_shared_object_exports_every_declared_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (tritd_\w+)", out))
+    missing = set(declared_symbols()) - exported
+    assert not missing, missing
+
+
+def test_library_is_gfx950_code(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib.LIB_PATH],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr
+
+
+def test_version_and_device_count(lib):
+    assert b"gfx950" in lib.lib.tritd_version()
+    assert lib.device_count() >= 0
+
+
+def _opts(lib, **kw):
+    o = lib.Opts()
+    o.mu, o.rho, o.lambda_, o.lambda2, o.tol, o.maxIter, o.disp = 1e-3, 1.25, 1.8, 1e-3, 1e-5, 5, 0
+    o.present = kw.get("present", 0x7F)
+    return o
+
+
+def test_missing_opts_field_is_reported_like_matlab(lib):
+    D = np.zeros((4, 4, 4), order="F")
+    o = _opts(lib, present=0x7F & ~lib.OPT_LAMBDA2)
+    buf = [np.zeros(64) for _ in range(3)]
+    st = lib.lib.tritd_admm_f64(C.c_void_p(D.ctypes.data), 4, 4, 4, 2, C.byref(o),
+                                *[C.c_void_p(b.ctypes.data) for b in buf], None, None, None, None,
+                                None, None, None, -1)
+    assert st == 2  # TRITD_ERR_OPTS
+    assert lib.lib.tritd_last_error() == b"Reference to non-existent field 'lambda2'."
+
+
+def test_python_api_raises_keyerror_for_missing_field():
+    import tritd
+    with pytest.raises(KeyError, match="non-existent field 'tol'"):
+        tritd.triple_decomp_ADMM(np.zeros((3, 3, 3)), 1,
+                                 dict(mu=1, rho=1, **{"lambda": 1}, lambda2=1, maxIter=1, disp=0))
+
+
+def test_rank_above_fp64_kernels_is_unsupported(lib):
+    D = np.zeros((4, 4, 4), order="F")
+    o = _opts(lib)
+    big = np.zeros(4 * 81 * 4)
+    st = lib.lib.tritd_admm_f64(C.c_void_p(D.ctypes.data), 4, 4, 4, 9, C.byref(o),
+                                *[C.c_void_p(big.ctypes.data)] * 3, None, None, None, None, None,
+                                None, None, -1)
+    assert st == 7  # TRITD_ERR_UNSUPPORTED
+
+
+def test_bad_unfold_mode_message(lib):
+    X = np.zeros(8)
+    st = lib.lib.tritd_unfold_f64(C.c_void_p(X.ctypes.data), 2, 2, 2, 4, C.c_void_p(X.ctypes.data))
+    assert st == 1
+    assert lib.lib.tritd_last_error() == b"Mode must be 1, 2, or 3."
+
+
+def test_no_cpu_fallback_without_gpu(lib):
+    import tritd
+    if tritd.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(tritd.TritdError, match="NODEV"):
+        tritd.soft_threshold(np.ones(4), 0.5)
+    with pytest.raises(tritd.TritdError, match="NODEV"):
+        from tritd import synth
+        d = synth.low_rank_plus_outliers(4, 4, 4, 2)
+        tritd.triple_decomp_ADMM(d["D"], 2, synth.TRAFFIC_OPTS, d["A0"], d["B0"], d["C0"])
+
+
+def test_shard_range_validation(lib):
+    o = _opts(lib)
+    D = np.zeros(64)
+    s = C.c_void_p()
+    st = lib.lib.tritd_session_create(C.byref(s), 0, C.c_void_p(D.ctypes.data), 4, 4, 4, 4, 3, 2,
+                                      2, C.byref(o), *[C.c_void_p(D.ctypes.data)] * 3, None, 0)
+    assert st == 1  # i0 >= i1
