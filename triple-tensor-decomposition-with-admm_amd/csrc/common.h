@@ -45,6 +45,9 @@ inline bool rp_supported(int RP) { return RP == 16 || RP == 32 || RP == 48 || RP
 //     (t%16 = (l>>4) + 4r, i%16 = l&15) sits at (r>>1)*128 + 2l + (r&1), so a
 //     wave reads/writes a tile as two fully contiguous 1 KB dwordx4 sweeps and
 //     walks its ij-tile's t-tiles as one contiguous stream.  Pads are zero.
+//     T alone uses the transposed in-tile order "TX": slot (s, l), at
+//     (s>>1)*128 + 2l + (s&1), holds (i%16 = 4s + (l>>4), t%16 = l&15) — the
+//     B-operand order of the mode-3 MFMA (k_contract.hip, K2).
 //   padded column-major ("PC") X[(t*n2 + j)*n1p + i] is used only at the
 //     host boundary and by the primitives.
 //   factors      Ah[i*RP+k], AhT[k*n1p+i], Bh[j*RP+k], Ch[t*RP+k], ChT[k*n3p+t]

@@ -84,6 +84,10 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     d2v* YO2 = reinterpret_cast<d2v*>(a.YO);
     d2v* T2 = reinterpret_cast<d2v*>(a.T);
 
+    // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
+    __shared__ double tsm[K5_WAVES][16 * 17];
+    double* ts = tsm[wid];
+
     if (active) {
         // register double buffer: [0] = D, [1] = Y_L, [2] = E (PRO: O), [3] = Y_O
         d2v nx[4][2];
@@ -116,15 +120,12 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
             if (PRO) {
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
-                    d2v tv;
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {
                         const double d = cx[0][p][q], yl = cx[1][p][q], ov = cx[2][p][q];
                         const double tn = (d - ov) + sc.invL * yl;  // :33
-                        tv[q] = tn;
                         tr[2 * p + q] = tn;
                     }
-                    T2[o + 64 * p] = tv;
                 }
             } else {
                 d4 lacc = {0.0, 0.0, 0.0, 0.0};
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
                 }
 #pragma unroll
                 for (int p = 0; p < 2; ++p) {
-                    d2v On2, En2, YLn2, YOn2, Tn2;
+                    d2v On2, En2, YLn2, YOn2;
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {
                         const int r = 2 * p + q;
@@ -158,16 +159,27 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
                         En2[q] = En;
                         YLn2[q] = YLn;
                         YOn2[q] = YOn;
-                        Tn2[q] = Tn;
                         tr[r] = Tn;
                     }
                     O2[o + 64 * p] = On2;
                     E2[o + 64 * p] = En2;
                     YL2[o + 64 * p] = YLn2;
                     YO2[o + 64 * p] = YOn2;
-                    T2[o + 64 * p] = Tn2;
                 }
             }
+            // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ts[(tg + 4 * r) * 17 + il] = tr[r];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                d2v tv;
+                tv[0] = ts[il * 17 + 4 * (2 * p) + tg];
+                tv[1] = ts[il * 17 + 4 * (2 * p + 1) + tg];
+                T2[o + 64 * p] = tv;
+            }
+            __builtin_amdgcn_wave_barrier();
             // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

@@ -85,166 +85,162 @@ void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, c
 }
 
 // ---------------------------------------------------------------------------
-// M3 partials: part[y][t][k] = sum over the block's ij-chunks of T(ij,t) KR(ij,k)
-//   grid.x = t-blocks of 64, grid.y = split index; chunk = 64 ij (4 ij-tiles)
-//   LDS: T tile [64 t][66] (pad 2 -> conflict-free ds_read_b64 of the B operand)
-//        KR tile [64 ij][SKR]  (SKR = RP or RP+16 so 2*SKR = 32 mod 64)
-//   MFMA: D(k, t) += sum_ij KR(ij,k) T(ij,t); K-step s covers ij = 4s..4s+3
-//   The next chunk's T is prefetched into registers during the MFMAs.
+// K2 — mode-3 MTTKRP  M3(t,k) = sum_ij T(ij,t) A^(i,k) B^(j,k)  (update_C, :93)
+//
+// T arrives in the "TX" fragment order written by K5 (common.h): for
+// ij-tile g and t-tile tt, lane l's two d2v hold T(ij = 16g + 4s + (l>>4),
+// t = 16tt + (l&15)) for s = 0..3 — exactly the B operand of
+// v_mfma_f64_16x16x4_f64 for the K-steps s of D(k,t) += KR(ij,k) T(ij,t).
+// So each wave streams T from HBM straight into registers (1 KB contiguous
+// per wave-instruction, next ij-tile prefetched), builds its KR operands
+// from L2-resident A^/B^ rows, and runs (RP/16)*4*4 MFMAs per ij-tile.
+// Wave = (t-block of 64 t, contiguous ij-tile range); the 4 waves of a
+// workgroup share the t-block and are summed through LDS in fixed order;
+// the per-workgroup partials are summed by k_m3_reduce in fixed order.
 // ---------------------------------------------------------------------------
-constexpr int M3_TS = 66;
-
-template <int RP>
-struct M3Cfg {
-    static constexpr int MT = RP / 16;
-    static constexpr int KSPLIT = (MT == 3) ? 1 : 4 / MT;  // waves sharing one k-tile
-    static constexpr int SKR = (RP % 32 == 0) ? RP + 16 : RP;
-    static constexpr int LDS_T = 64 * M3_TS;
-    static constexpr int LDS_KR = 64 * SKR;
-};
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 template <int RP>
 __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
                                                const double* __restrict__ Ah,
                                                const double* __restrict__ Bh, double* part,
                                                int64_t n1p, int64_t n3p, int64_t ntt,
-                                               int64_t tiles, int split, const int* stop) {
+                                               int64_t tiles, int S, const int* stop) {
     if (*stop) return;
-    using C = M3Cfg<RP>;
+    constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* sT = lds;             // [64][M3_TS]
-    double* sK = lds + C::LDS_T;  // [64][SKR]
-
-    const int th = threadIdx.x, lane = th & 63, wid = th >> 6;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int il = lane & 15, tg = lane >> 4;
-    const int64_t t0 = (int64_t)blockIdx.x * 64;
-    const int64_t nchunk = cdiv(tiles, 4);
+    const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t tb = wave / S;
+    const int64_t sidx = wave - tb * S;
+    const int64_t g0 = tiles * sidx / S, g1 = tiles * (sidx + 1) / S;
     const int64_t qper = n1p >> 4;
-
-    const int mt = (C::MT == 3) ? wid : wid % C::MT;
-    const int kpart = (C::MT == 3) ? 0 : wid / C::MT;
-    const bool wave_on = wid < C::MT * C::KSPLIT;
-
-    d4 acc[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
-
-    // T staging from the tile-major layout: the chunk's 4 ij-tiles x the
-    // block's 4 t-tiles are 16 contiguous 2 KB tiles = 2048 d2v; thread th in
-    // round m takes d2v idx = m*256 + th (1 KB contiguous per wave-instruction)
-    typedef double d2v __attribute__((ext_vector_type(2)));
     const d2v* T2 = reinterpret_cast<const d2v*>(T);
-    d2v pre[8];
-    auto load_T = [&](int64_t c) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int idx = m * 256 + th;
-            const int q = idx >> 7, w = idx & 127;
-            const int64_t g = c * 4 + (q & 3), tt = (int64_t)blockIdx.x * 4 + (q >> 2);
-            if (g < tiles && tt < ntt)
-                pre[m] = T2[(g * ntt + tt) * 128 + w];
-            else
-                pre[m] = d2v{0.0, 0.0};
-        }
-    };
-    auto store_T = [&]() {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int idx = m * 256 + th;
-            const int q = idx >> 7, w = idx & 127;
-            const int gi = q & 3, ti = q >> 2, p = w >> 6, l = w & 63;
-            const int row = 16 * ti + (l >> 4) + 8 * p, col = 16 * gi + (l & 15);
-            sT[row * M3_TS + col] = pre[m][0];        // r = 2p
-            sT[(row + 4) * M3_TS + col] = pre[m][1];  // r = 2p + 1
-        }
-    };
 
-    int64_t c = blockIdx.y;
-    if (c < nchunk) load_T(c);
-    for (; c < nchunk; c += split) {
-        __syncthreads();  // previous chunk's LDS reads are done
-        store_T();
-        // KR tile: entry e -> (ij = e / RP, k = e % RP)
-        for (int e = th; e < 64 * RP; e += 256) {
-            const int ijl = e / RP, k = e - ijl * RP;
-            const int64_t tile = c * 4 + (ijl >> 4);
-            double v = 0.0;
-            if (tile < tiles) {
-                const int64_t j = tile / qper;
-                const int64_t i = ((tile - j * qper) << 4) + (ijl & 15);
-                v = Ah[i * RP + k] * Bh[j * RP + k];
-            }
-            sK[ijl * C::SKR + k] = v;
-        }
-        __syncthreads();
-        if (c + split < nchunk) load_T(c + split);  // prefetch, lands during the MFMAs
-        if (wave_on) {
-#pragma unroll 4
-            for (int s = kpart; s < 16; s += C::KSPLIT) {
-                const double av = sK[(4 * s + tg) * C::SKR + 16 * mt + il];
+    d4 acc[MT][4];
 #pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const double bv = sT[(16 * n + il) * M3_TS + 4 * s + tg];
-                    acc[n] = mfma4(av, bv, acc[n]);
-                }
-            }
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = d4{0.0, 0.0, 0.0, 0.0};
+
+    d2v nb[4][2];
+    auto loadB = [&](int64_t g) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int64_t tt = tb * 4 + n;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                nb[n][p] = (tt < ntt) ? T2[(g * ntt + tt) * 128 + 64 * p + lane] : d2v{0.0, 0.0};
+        }
+    };
+    if (g0 < g1) loadB(g0);
+    for (int64_t g = g0; g < g1; ++g) {
+        d2v b[4][2];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            b[n][0] = nb[n][0];
+            b[n][1] = nb[n][1];
+        }
+        if (g + 1 < g1) loadB(g + 1);
+        const int64_t j = g / qper;
+        const int64_t i0 = (g - j * qper) << 4;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const int k = 16 * m + il;
+            const double bh = Bh[j * RP + k];
+            double a[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) a[s] = Ah[(i0 + 4 * s + tg) * RP + k] * bh;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int n = 0; n < 4; ++n) acc[m][n] = mfma4(a[s], b[n][s >> 1][s & 1], acc[m][n]);
         }
     }
 
-    // combine the KSPLIT waves that share a k-tile (fixed order), write partial
+    // fixed-order sum of the 4 waves: (w2,w3) -> (w0,w1), then w1 -> w0
+    constexpr int PER = MT * 16;  // doubles per lane
+    if (wid >= 2) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    lds[((wid - 2) * PER + (m * 4 + n) * 4 + rr) * 64 + lane] = acc[m][n][rr];
+    }
     __syncthreads();
-    double* red = lds;  // reuse: [4 waves][4 n][4 rr][64 lanes]
-    if (C::KSPLIT > 1) {
+    if (wid < 2) {
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) red[((wid * 4 + n) * 4 + rr) * 64 + lane] = acc[n][rr];
-        __syncthreads();
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    acc[m][n][rr] += lds[(wid * PER + (m * 4 + n) * 4 + rr) * 64 + lane];
     }
-    if (wave_on && kpart == 0) {
-        double* out = part + (int64_t)blockIdx.y * n3p * RP;
+    __syncthreads();
+    if (wid == 1) {
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                double v = acc[n][rr];
-                if (C::KSPLIT > 1)
-                    for (int q = 1; q < C::KSPLIT; ++q)
-                        v += red[(((wid + q * C::MT) * 4 + n) * 4 + rr) * 64 + lane];
-                const int64_t t = t0 + 16 * n + il;
-                const int k = 16 * mt + tg + 4 * rr;
-                if (t < n3p) out[t * RP + k] = v;
-            }
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) lds[((m * 4 + n) * 4 + rr) * 64 + lane] = acc[m][n][rr];
+    }
+    __syncthreads();
+    if (wid == 0) {
+        double* out = part + (int64_t)(sidx >> 2) * n3p * RP;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const double v = acc[m][n][rr] + lds[((m * 4 + n) * 4 + rr) * 64 + lane];
+                    const int64_t t = tb * 64 + 16 * n + il;
+                    const int k = 16 * m + tg + 4 * rr;
+                    if (t < n3p) out[t * RP + k] = v;
+                }
     }
 }
 
-// M3[t][k] = sum_y part[y][t][k]  (fixed order)
+// M3[t][k] = sum_y part[y][t][k]  (fixed order); 4 slices per output summed in LDS
 __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ part, double* M3,
-                                                   int64_t count, int split, const int* stop) {
+                                                   int64_t count, int nparts, const int* stop) {
     if (*stop) return;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= count) return;
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
     double s = 0.0;
-    for (int y = 0; y < split; ++y) s += part[(int64_t)y * count + e];
-    M3[e] = s;
+    if (e < count)
+        for (int y = q; y < nparts; y += 4) s += part[(int64_t)y * count + e];
+    __shared__ double red[4][64];
+    red[q][lane] = s;
+    __syncthreads();
+    if (q == 0 && e < count) M3[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// waves per t-block (multiple of 4): about two waves per SIMD in total
 int m3_split(const Geom& g) {
-    const int64_t nchunk = cdiv(g.tiles, 4);
-    const int64_t tb = cdiv(g.n3p, 64);
-    int64_t split = cdiv(512, tb);  // ~2 workgroups per CU
-    if (split > nchunk) split = nchunk;
-    if (split < 1) split = 1;
-    return (int)split;
+    const int64_t ntb = cdiv(g.ntt, 4);
+    int64_t S = 2048 / ntb;
+    if (S > g.tiles) S = g.tiles;
+    S = (S + 3) / 4 * 4;
+    if (S < 4) S = 4;
+    return (int)S;
 }
+
+int m3_parts(const Geom& g) { return m3_split(g) / 4; }
 
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
                double* M3, const int* stop, hipStream_t st) {
-    const int split = m3_split(g);
-    const dim3 grid((unsigned)cdiv(g.n3p, 64), (unsigned)split);
+    const int S = m3_split(g);
+    const int64_t ntb = cdiv(g.ntt, 4);
+    const dim3 grid((unsigned)(ntb * S / 4));
 #define M3_CASE(RPV)                                                                          \
     case RPV: {                                                                               \
-        const size_t lds = (M3Cfg<RPV>::LDS_T + M3Cfg<RPV>::LDS_KR) * sizeof(double);         \
+        const size_t lds = (size_t)2 * (RPV / 16) * 16 * 64 * sizeof(double);                \
         static bool attr_set = false;                                                         \
         if (!attr_set) {                                                                      \
             TRITD_HIP(hipFuncSetAttribute((const void*)k_m3<RPV>,                             \
@@ -252,7 +248,7 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
             attr_set = true;                                                                  \
         }                                                                                     \
         hipLaunchKernelGGL(k_m3<RPV>, grid, dim3(256), lds, st, T, Ah, Bh, part, g.n1p, g.n3p, \
-                           g.ntt, g.tiles, split, stop);                                    \
+                           g.ntt, g.tiles, S, stop);                                          \
     } break;
     switch (g.RP) {
         M3_CASE(16)
@@ -265,8 +261,8 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
 #undef M3_CASE
     TRITD_CHECK_LAUNCH();
     const int64_t count = g.n3p * g.RP;
-    hipLaunchKernelGGL(k_m3_reduce, dim3((unsigned)cdiv(count, 256)), dim3(256), 0, st, part, M3,
-                       count, split, stop);
+    hipLaunchKernelGGL(k_m3_reduce, dim3((unsigned)cdiv(count, 64)), dim3(256), 0, st, part, M3,
+                       count, m3_parts(g), stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -308,63 +304,79 @@ void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* st
 }
 
 // ---------------------------------------------------------------------------
-// Ginv = inv(P o Q + alpha I): in-place Gauss-Jordan in LDS, one block,
-// thread (column c = th&63, rows h, h+4, ...).  The Gram is SPD (ridge
-// alpha > 0) so no pivoting is needed; the smallest Gauss-Jordan pivot
-// (= smallest LDL^T pivot) is compared with MATLAB's pinv tolerance
-// max(size)*eps(max sigma) and flags[0] is raised when pinv could truncate
-// (triple_decomp_ADMM.m:78,86,93 use pinv).
+// Ginv = inv(P o Q + alpha I): in-place Gauss-Jordan in LDS, one block.
+// The R x R Gram is embedded in an RP x RP matrix with an identity pad, so
+// every thread runs the same branch-free code: thread (column c = th % RP,
+// rows h + G*m).  Two LDS copies ping-pong between pivots, so one barrier
+// per pivot suffices.  The Gram is SPD (ridge alpha > 0): no pivoting.  The
+// smallest Gauss-Jordan pivot (= smallest LDL^T pivot) is compared with
+// MATLAB's pinv tolerance max(size)*eps(max sigma); flags[0] is raised when
+// pinv could truncate (triple_decomp_ADMM.m:78,86,93 use pinv).
 // ---------------------------------------------------------------------------
+template <int RP>
+struct SolveCfg {
+    static constexpr int NT = (RP == 48) ? 192 : 256;  // threads
+    static constexpr int G = NT / RP;                  // row groups
+    static constexpr int RPT = RP / G;                 // rows per thread
+    static constexpr int LD = RP + 1;
+};
+
+template <int RP>
 __global__ __launch_bounds__(256) void k_solve(const double* __restrict__ P,
-                                               const double* __restrict__ Q, int RP, int R,
-                                               double alpha, double* Ginv, int* flags,
-                                               const int* stop) {
+                                               const double* __restrict__ Q, int R, double alpha,
+                                               double* Ginv, int* flags, const int* stop) {
     if (*stop) return;
-    __shared__ double M[64][65];
+    using S = SolveCfg<RP>;
+    constexpr int G = S::G, RPT = S::RPT, LD = S::LD;
+    __shared__ double M[2][RP * LD];
     const int th = threadIdx.x;
-    const int c = th & 63, h = th >> 6;
-    const bool colok = c < R;
+    const int c = th % RP, h = th / RP;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const int i = h + 4 * m;
-        if (i < R && colok) {
-            double v = P[i * RP + c] * Q[i * RP + c];
+    for (int m = 0; m < RPT; ++m) {
+        const int i = h + G * m;
+        double v;
+        if (i < R && c < R) {
+            v = P[i * RP + c] * Q[i * RP + c];
             if (i == c) v = v + alpha;
-            M[i][c] = v;
+        } else {
+            v = (i == c) ? 1.0 : 0.0;
         }
+        M[0][i * LD + c] = v;
     }
     __syncthreads();
     double minpiv = 1e308, maxpiv = 0.0;
-    for (int p = 0; p < R; ++p) {
-        const double piv = M[p][p];
-        minpiv = fmin(minpiv, piv);
-        maxpiv = fmax(maxpiv, piv);
-        const double d = 1.0 / piv;
-        const double prv = colok ? ((c == p) ? d : M[p][c] * d) : 0.0;  // new pivot row
-        double f[16];
+    for (int p = 0; p < RP; ++p) {
+        const double* src = M[p & 1];
+        double* dst = M[(p + 1) & 1];
+        const double piv = src[p * LD + p];
+        const double mpc = src[p * LD + c];
+        double mv[RPT], f[RPT];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            const int i = h + 4 * m;
-            f[m] = (i < R) ? M[i][p] : 0.0;
+        for (int m = 0; m < RPT; ++m) {
+            const int i = h + G * m;
+            mv[m] = src[i * LD + c];
+            f[m] = src[i * LD + p];
         }
-        __syncthreads();
-        if (colok) {
+        if (p < R) {
+            minpiv = fmin(minpiv, piv);
+            maxpiv = fmax(maxpiv, piv);
+        }
+        const double d = 1.0 / piv;
+        const double prv = (c == p) ? d : mpc * d;  // new pivot row
 #pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                const int i = h + 4 * m;
-                if (i < R) {
-                    if (i == p)
-                        M[i][c] = prv;
-                    else
-                        M[i][c] = ((c == p) ? 0.0 : M[i][c]) - f[m] * prv;
-                }
-            }
+        for (int m = 0; m < RPT; ++m) {
+            const int i = h + G * m;
+            const double base = (c == p) ? 0.0 : mv[m];
+            const double upd = base - f[m] * prv;
+            dst[i * LD + c] = (i == p) ? prv : upd;
         }
         __syncthreads();
     }
-    for (int e = th; e < RP * RP; e += 256) {
-        const int i = e / RP, cc = e - i * RP;
-        Ginv[e] = (i < R && cc < R) ? M[i][cc] : 0.0;
+    const double* fin = M[RP & 1];
+#pragma unroll
+    for (int m = 0; m < RPT; ++m) {
+        const int i = h + G * m;
+        Ginv[i * RP + c] = (i < R && c < R) ? fin[i * LD + c] : 0.0;
     }
     if (th == 0) {
         // eps(x) = 2^(floor(log2 x) - 52)
@@ -375,8 +387,20 @@ __global__ __launch_bounds__(256) void k_solve(const double* __restrict__ P,
 
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
                   int* flags, const int* stop, hipStream_t st) {
-    if (R > 64) throw Error(TRITD_ERR_UNSUPPORTED, "R > 64 solve");
-    hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), 0, st, P, Q, RP, R, alpha, Ginv, flags, stop);
+#define SOLVE_CASE(RPV)                                                                      \
+    case RPV:                                                                                \
+        hipLaunchKernelGGL(k_solve<RPV>, dim3(1), dim3(SolveCfg<RPV>::NT), 0, st, P, Q, R, alpha, \
+                           Ginv, flags, stop);                                               \
+        break;
+    switch (RP) {
+        SOLVE_CASE(16)
+        SOLVE_CASE(32)
+        SOLVE_CASE(48)
+        SOLVE_CASE(64)
+        default:
+            throw Error(TRITD_ERR_UNSUPPORTED, "R > 64 solve");
+    }
+#undef SOLVE_CASE
     TRITD_CHECK_LAUNCH();
 }
 

@@ -42,6 +42,7 @@ void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, co
 void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, const int* stop,
                hipStream_t st);
 int m3_split(const Geom& g);
+int m3_parts(const Geom& g);  // partial slabs of n3p*RP written by K2
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
                double* M3, const int* stop, hipStream_t st);
 // G = X^T X over `rows` rows of a row-major [rows][RP] factor

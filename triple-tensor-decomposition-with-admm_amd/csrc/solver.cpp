@@ -115,7 +115,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     red2_.alloc(red2_count());
     red3_.alloc(2);
     k5part_.alloc(2 * (size_t)k5_grid(g_));
-    m3part_.alloc((size_t)m3_split(g_) * g_.n3p * g_.RP);
+    m3part_.alloc((size_t)m3_parts(g_) * g_.n3p * g_.RP);
     sqpart_.alloc(2 * (size_t)sumsq_blocks(g_));
     const size_t mi = o_.maxIter > 0 ? (size_t)o_.maxIter : 1;
     errHist_.alloc(mi);
