@@ -49,6 +49,7 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     if (*a.stop) return;
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
+    constexpr int LDC = RP + 16; // row stride of the [t][k] C^ slice (2*LDC = 32 mod 64: no bank conflicts)
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int il = lane & 15;
@@ -62,6 +63,27 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     // this lane's d2v slots inside the wave's stream: tile tt, pair p at
     // stream + tt*128 + p*64 + lane   (in units of d2v)
     const int64_t sbase = tile * ntt * 128 + lane;
+
+    // C^ rows of one t-tile, staged once per workgroup (double buffered):
+    //   sCT[k][16]  (L operand: C^(t0+l&15, 4s+(l>>4)))
+    //   sC [16][LDC] (W operand: C^(t0+4r+(l>>4), 16m+(l&15)))
+    __shared__ double sCT[2][RP * 16];
+    __shared__ double sC[2][16 * LDC];
+    // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
+    __shared__ double tsm[K5_WAVES][16 * 17];
+    double* ts = tsm[wid];
+    auto stage = [&](int64_t tt, int buf) {
+        // 16 rows x RP of Ch (row-major [t][RP]), 2 doubles per thread-step
+        for (int e = threadIdx.x; e < 16 * RP / 2; e += 64 * K5_WAVES) {
+            const int row = (2 * e) / RP, k = (2 * e) % RP;
+            const double* src = a.Ch + ((tt << 4) + row) * RP + k;
+            const double v0 = src[0], v1 = src[1];
+            sC[buf][row * LDC + k] = v0;
+            sC[buf][row * LDC + k + 1] = v1;
+            sCT[buf][k * 16 + row] = v0;
+            sCT[buf][(k + 1) * 16 + row] = v1;
+        }
+    };
 
     double kr[KS];
     if (!PRO) {
@@ -84,94 +106,99 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     d2v* YO2 = reinterpret_cast<d2v*>(a.YO);
     d2v* T2 = reinterpret_cast<d2v*>(a.T);
 
-    // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
-    __shared__ double tsm[K5_WAVES][16 * 17];
-    double* ts = tsm[wid];
-
-    if (active) {
-        // register double buffer: [0] = D, [1] = Y_L, [2] = E (PRO: O), [3] = Y_O
-        d2v nx[4][2];
-        auto load = [&](int64_t tt) {
-            const int64_t o = sbase + tt * 128;
+    // register double buffer: [0] = D, [1] = Y_L, [2] = E (PRO: O), [3] = Y_O
+    d2v nx[4][2];
+    auto load = [&](int64_t tt) {
+        if (!active) return;
+        const int64_t o = sbase + tt * 128;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            nx[0][p] = D2[o + 64 * p];
+            nx[1][p] = YL2[o + 64 * p];
+            if (PRO) {
+                nx[2][p] = O2[o + 64 * p];
+            } else {
+                nx[2][p] = E2[o + 64 * p];
+                nx[3][p] = YO2[o + 64 * p];
+            }
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nx[q][0] = nx[q][1] = d2v{0.0, 0.0};
+    load(0);
+    stage(0, 0);
+    __syncthreads();
+    for (int64_t tt = 0; tt < ntt; ++tt) {
+        const int buf = (int)(tt & 1);
+        d2v cx[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            cx[q][0] = nx[q][0];
+            cx[q][1] = nx[q][1];
+        }
+        if (tt + 1 < ntt) {
+            load(tt + 1);
+            stage(tt + 1, buf ^ 1);
+        }
+        const int64_t o = sbase + tt * 128;
+        const double* cT = sCT[buf];
+        const double* cR = sC[buf];
+        double tr[4];
+        if (PRO) {
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                nx[0][p] = D2[o + 64 * p];
-                nx[1][p] = YL2[o + 64 * p];
-                if (PRO) {
-                    nx[2][p] = O2[o + 64 * p];
-                } else {
-                    nx[2][p] = E2[o + 64 * p];
-                    nx[3][p] = YO2[o + 64 * p];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double d = cx[0][p][q], yl = cx[1][p][q], ov = cx[2][p][q];
+                    const double tn = (d - ov) + sc.invL * yl;  // :33
+                    tr[2 * p + q] = tn;
                 }
             }
-        };
-        load(0);
-        for (int64_t tt = 0; tt < ntt; ++tt) {
-            d2v cx[4][2];
+        } else {
+            d4 lacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                cx[q][0] = nx[q][0];
-                cx[q][1] = nx[q][1];
-            }
-            if (tt + 1 < ntt) load(tt + 1);
-            const int64_t t0 = tt << 4;
-            const int64_t o = sbase + tt * 128;
-            double tr[4];
-            if (PRO) {
+            for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
 #pragma unroll
-                for (int p = 0; p < 2; ++p) {
+            for (int p = 0; p < 2; ++p) {
+                d2v On2, En2, YLn2, YOn2;
 #pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        const double d = cx[0][p][q], yl = cx[1][p][q], ov = cx[2][p][q];
-                        const double tn = (d - ov) + sc.invL * yl;  // :33
-                        tr[2 * p + q] = tn;
-                    }
+                for (int q = 0; q < 2; ++q) {
+                    const int r = 2 * p + q;
+                    const double d = cx[0][p][q], yl = cx[1][p][q], e = cx[2][p][q],
+                                 yo = cx[3][p][q];
+                    const double L = lacc[r];
+                    const double R1 = (d - L) + sc.invL * yl;               // :41
+                    const double R2 = e - sc.invO * yo;                     // :42
+                    const double On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
+                    const double R3 = On + sc.invO * yo;                    // :46
+                    const double En = matlab_sign(R3) * fmax(fabs(R3) - sc.thr, 0.0);  // :47
+                    const double rL = (d - L) - On;                         // :50
+                    const double rO = On - En;                              // :51
+                    const double YLn = yl + sc.muL * rL;                    // :52
+                    const double YOn = yo + sc.muO * rO;                    // :53
+                    const double Tn = (d - On) + sc.invL_next * YLn;        // :33 (k+1)
+                    ssL += rL * rL;
+                    ssO += rO * rO;
+                    On2[q] = On;
+                    En2[q] = En;
+                    YLn2[q] = YLn;
+                    YOn2[q] = YOn;
+                    tr[r] = Tn;
                 }
-            } else {
-                d4 lacc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int s = 0; s < KS; ++s) {
-                    const double c = a.ChT[(int64_t)(4 * s + tg) * a.n3p + t0 + il];
-                    lacc = mfma4(c, kr[s], lacc);
-                }
-#pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    d2v On2, En2, YLn2, YOn2;
-#pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        const int r = 2 * p + q;
-                        const double d = cx[0][p][q], yl = cx[1][p][q], e = cx[2][p][q],
-                                     yo = cx[3][p][q];
-                        const double L = lacc[r];
-                        const double R1 = (d - L) + sc.invL * yl;               // :41
-                        const double R2 = e - sc.invO * yo;                     // :42
-                        const double On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
-                        const double R3 = On + sc.invO * yo;                    // :46
-                        const double En = matlab_sign(R3) * fmax(fabs(R3) - sc.thr, 0.0);  // :47
-                        const double rL = (d - L) - On;                         // :50
-                        const double rO = On - En;                              // :51
-                        const double YLn = yl + sc.muL * rL;                    // :52
-                        const double YOn = yo + sc.muO * rO;                    // :53
-                        const double Tn = (d - On) + sc.invL_next * YLn;        // :33 (k+1)
-                        ssL += rL * rL;
-                        ssO += rO * rO;
-                        On2[q] = On;
-                        En2[q] = En;
-                        YLn2[q] = YLn;
-                        YOn2[q] = YOn;
-                        tr[r] = Tn;
-                    }
+                if (active) {
                     O2[o + 64 * p] = On2;
                     E2[o + 64 * p] = En2;
                     YL2[o + 64 * p] = YLn2;
                     YO2[o + 64 * p] = YOn2;
                 }
             }
-            // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
+        }
+        // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ts[(tg + 4 * r) * 17 + il] = tr[r];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int r = 0; r < 4; ++r) ts[(tg + 4 * r) * 17 + il] = tr[r];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (active) {
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 d2v tv;
@@ -179,15 +206,17 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
                 tv[1] = ts[il * 17 + 4 * (2 * p + 1) + tg];
                 T2[o + 64 * p] = tv;
             }
-            __builtin_amdgcn_wave_barrier();
-            // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double* crow = a.Ch + (t0 + 4 * r + tg) * RP + il;
-#pragma unroll
-                for (int m = 0; m < MT; ++m) wacc[m] = mfma4(crow[16 * m], tr[r], wacc[m]);
-            }
         }
+        // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                wacc[m] = mfma4(cR[(4 * r + tg) * LDC + 16 * m + il], tr[r], wacc[m]);
+        }
+        __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
+    }
+    if (active) {
         // W^T C/D layout: row k = 16m + tg + 4rr, col ij = il
         const int64_t wbase = (tile << 4) + il;
 #pragma unroll

@@ -30,21 +30,21 @@ __global__ __launch_bounds__(256) void k_m1(const double* __restrict__ Wk,
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * 64 + lane;
     const int k = blockIdx.y;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    double acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = 0.0;
     if (i < n1p) {
         const double* wp = Wk + (int64_t)k * plane + i;
         const double* bp = Bh + k;
         int64_t j = w;
-        for (; j + 12 < n2; j += 16) {  // 4 independent chains, j = w + 4m
-            a0 = fma(wp[j * n1p], bp[j * RP], a0);
-            a1 = fma(wp[(j + 4) * n1p], bp[(j + 4) * RP], a1);
-            a2 = fma(wp[(j + 8) * n1p], bp[(j + 8) * RP], a2);
-            a3 = fma(wp[(j + 12) * n1p], bp[(j + 12) * RP], a3);
+        for (; j + 28 < n2; j += 32) {  // 8 independent chains, j = w + 4u
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] = fma(wp[(j + 4 * u) * n1p], bp[(j + 4 * u) * RP], acc[u]);
         }
-        for (; j < n2; j += 4) a0 = fma(wp[j * n1p], bp[j * RP], a0);
+        for (; j < n2; j += 4) acc[0] = fma(wp[j * n1p], bp[j * RP], acc[0]);
     }
     __shared__ double red[4][64];
-    red[w][lane] = (a0 + a1) + (a2 + a3);
+    red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     __syncthreads();
     if (w == 0 && i < n1p) M1[i * RP + k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
@@ -269,26 +269,22 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
 // ---------------------------------------------------------------------------
 // Gram: G[k][k'] = sum_i X[i][k] X[i][k'] (rows in 256/RP interleaved groups)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gram(const double* __restrict__ X, int64_t rows, int RP,
-                                              double* G, const int* stop) {
+__global__ __launch_bounds__(1024) void k_gram(const double* __restrict__ X, int64_t rows, int RP,
+                                               double* G, const int* stop) {
     if (stop && *stop) return;
     const int k = blockIdx.x;
-    const int groups = 256 / RP;
+    const int groups = 1024 / RP;
     const int kk = threadIdx.x % RP, grp = threadIdx.x / RP;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    if (grp < groups) {
-        const int64_t st = groups;
-        int64_t i = grp;
-        for (; i + 3 * st < rows; i += 4 * st) {
-            a0 = fma(X[i * RP + k], X[i * RP + kk], a0);
-            a1 = fma(X[(i + st) * RP + k], X[(i + st) * RP + kk], a1);
-            a2 = fma(X[(i + 2 * st) * RP + k], X[(i + 2 * st) * RP + kk], a2);
-            a3 = fma(X[(i + 3 * st) * RP + k], X[(i + 3 * st) * RP + kk], a3);
-        }
-        for (; i < rows; i += st) a0 = fma(X[i * RP + k], X[i * RP + kk], a0);
+    double a0 = 0.0, a1 = 0.0;
+    const int64_t st = groups;
+    int64_t i = grp;
+    for (; i + st < rows; i += 2 * st) {
+        a0 = fma(X[i * RP + k], X[i * RP + kk], a0);
+        a1 = fma(X[(i + st) * RP + k], X[(i + st) * RP + kk], a1);
     }
-    __shared__ double red[256];
-    red[threadIdx.x] = (a0 + a1) + (a2 + a3);
+    if (i < rows) a0 = fma(X[i * RP + k], X[i * RP + kk], a0);
+    __shared__ double red[1024];
+    red[threadIdx.x] = a0 + a1;
     __syncthreads();
     if (grp == 0) {
         double s = red[kk];
@@ -299,7 +295,7 @@ __global__ __launch_bounds__(256) void k_gram(const double* __restrict__ X, int6
 
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_gram, dim3(RP), dim3(256), 0, st, X, rows, RP, G, stop);
+    hipLaunchKernelGGL(k_gram, dim3(RP), dim3(1024), 0, st, X, rows, RP, G, stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -412,14 +408,25 @@ __global__ __launch_bounds__(256) void k_apply(const double* __restrict__ M, int
                                                double* YT, int64_t ldT, const int* stop) {
     if (stop && *stop) return;
     __shared__ double g[64 * 64];
+    __shared__ double m[16 * 65];
+    const int64_t r0 = (int64_t)blockIdx.x * 16;
     for (int e = threadIdx.x; e < RP * RP; e += 256) g[e] = Ginv[e];
+    for (int e = threadIdx.x; e < 16 * RP; e += 256) {
+        const int rr = e / RP, q = e - rr * RP;
+        m[rr * 65 + q] = (r0 + rr < rows) ? M[(r0 + rr) * RP + q] : 0.0;
+    }
     __syncthreads();
     const int rpb = 256 / RP;  // rows per pass
     const int k = threadIdx.x % RP, rl = threadIdx.x / RP;
-    for (int64_t i = (int64_t)blockIdx.x * 16 + rl; i < (int64_t)blockIdx.x * 16 + 16; i += rpb) {
+    for (int rr = rl; rr < 16; rr += rpb) {
+        const int64_t i = r0 + rr;
         if (i >= rows) break;
-        double s = 0.0;
-        for (int q = 0; q < RP; ++q) s = fma(M[i * RP + q], g[q * RP + k], s);
+        double s0 = 0.0, s1 = 0.0;
+        for (int q = 0; q < RP; q += 2) {
+            s0 = fma(m[rr * 65 + q], g[q * RP + k], s0);
+            s1 = fma(m[rr * 65 + q + 1], g[(q + 1) * RP + k], s1);
+        }
+        const double s = s0 + s1;
         Y[i * RP + k] = s;
         if (YT) YT[(int64_t)k * ldT + i] = s;
     }

@@ -12,6 +12,7 @@
 #include "solver.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace tritd {
@@ -82,6 +83,17 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         own_stream_ = true;
     }
     g_ = make_geom(n1, n2, n3, i0, i1, r);
+    overlap_ = (comm == nullptr) && (shared_stream == nullptr);
+    {
+        const char* ov = std::getenv("TRITD_OVERLAP");
+        ovmode_ = ov ? std::atoi(ov) : 2;
+        if (ovmode_ == 0) overlap_ = false;
+    }
+    if (overlap_) {
+        TRITD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&evAtA_, &evBtB_, &evCtC_, &evSA_, &evSB_, &evSC_})
+            TRITD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
     if (!rp_supported(g_.RP)) throw Error(TRITD_ERR_UNSUPPORTED, "r must be in 1..8 for the fp64 path");
 
     // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
@@ -96,9 +108,22 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     }
 
     const size_t Np = (size_t)g_.Np;
-    for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
-        b->alloc(Np);
-        TRITD_HIP(hipMemsetAsync(b->p, 0, Np * sizeof(double), st_));
+    {
+        // the six streamed tensors live in one pool; each base is staggered so
+        // that equal offsets of concurrently streamed tensors do not map to
+        // the same HBM channel
+        const char* sg = std::getenv("TRITD_STAGGER");
+        const size_t stagger = sg ? (size_t)std::atoll(sg) : 256;  // measured: tools/stagger_sweep.py
+        const size_t slot = round_up((int64_t)(Np * sizeof(double) + 5 * stagger), 4096);
+        pool_.alloc(6 * slot / sizeof(double));
+        int q = 0;
+        for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
+            b->p = pool_.p + (q * slot + q * stagger) / sizeof(double);
+            b->n = Np;
+            b->owned = false;
+            TRITD_HIP(hipMemsetAsync(b->p, 0, Np * sizeof(double), st_));
+            ++q;
+        }
     }
     Wk_.alloc((size_t)g_.RP * g_.plane);
     TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.n * sizeof(double), st_));
@@ -109,6 +134,11 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     ChT_.alloc((size_t)g_.RP * g_.n3p);
     M1_.alloc(g_.n1p * g_.RP);
     Ginv_.alloc((size_t)g_.RP * g_.RP);
+    if (overlap_) {
+        GinvA_.alloc((size_t)g_.RP * g_.RP);
+        GinvB_.alloc((size_t)g_.RP * g_.RP);
+        GinvC_.alloc((size_t)g_.RP * g_.RP);
+    }
     BtB_.alloc((size_t)g_.RP * g_.RP);
     CtC_.alloc((size_t)g_.RP * g_.RP);
     red1_.alloc(red1_count());
@@ -164,12 +194,25 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     a.s = scalars(1);
     a.stop = ctrl_;
     if (o_.maxIter > 0) launch_k5(g_, a, /*prologue=*/true, st_);
+    if (overlap_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
+        TRITD_HIP(hipEventRecord(evCtC_, st_));
+        TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
+        launch_solve(g_.RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+        TRITD_HIP(hipEventRecord(evSA_, side_));
+        TRITD_HIP(hipStreamSynchronize(side_));
+    }
     TRITD_HIP(hipStreamSynchronize(st_));
 }
 
 Session::~Session() {
     (void)hipSetDevice(device_);
     if (st_) (void)hipStreamSynchronize(st_);
+    if (side_) {
+        (void)hipStreamSynchronize(side_);
+        (void)hipStreamDestroy(side_);
+    }
+    for (hipEvent_t e : {evAtA_, evBtB_, evCtC_, evSA_, evSB_, evSC_})
+        if (e) (void)hipEventDestroy(e);
     for (auto e : ev_) (void)hipEventDestroy(e);
     if (ctrl_) (void)hipFree(ctrl_);
     if (own_stream_ && st_) (void)hipStreamDestroy(st_);
@@ -249,6 +292,10 @@ void Session::phaseC(int k) {
     launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :93 ridge
     launch_apply(RP, red2_.p, g_.n3p, Ginv_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    launch_k5_full(k);
+}
+
+void Session::launch_k5_full(int k) {
     K5Args a{};
     a.D = D_.p; a.O = O_.p; a.E = E_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
@@ -260,6 +307,49 @@ void Session::phaseC(int k) {
     launch_k5(g_, a, /*prologue=*/false, st_);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 2], st_));
     launch_reduce_pairs(k5part_.p, k5_grid(g_), red3_.p, ctrl_, st_);
+}
+
+// Single-GPU iteration.  Same kernels and data flow as phases A-D, but each
+// R x R solve runs on the side stream as soon as its Grams exist:
+//   solve B (A^TA, C^TC) || M2        solve C (A^TA, B^TB) || M3
+//   solve A of k+1 (B^TB, C^TC) || K5
+// Every buffer a side kernel reads is next written on the main stream only
+// after an event the side stream records behind that kernel.
+void Session::iterate_overlapped(int k) {
+    const int RP = g_.RP;
+    double* M2 = red1_.p;
+    double* AtA = red1_.p + g_.n2 * RP;
+    launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    if (ovmode_ == 1) launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, st_);
+    TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
+    launch_apply(RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    TRITD_HIP(hipEventRecord(evAtA_, st_));
+    TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
+    launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, GinvB_.p, ctrl_ + 2, ctrl_, side_);
+    TRITD_HIP(hipEventRecord(evSB_, side_));
+    launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
+    TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
+    launch_apply(RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, ctrl_, st_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    TRITD_HIP(hipEventRecord(evBtB_, st_));
+    TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
+    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, side_);  // :93 ridge
+    TRITD_HIP(hipEventRecord(evSC_, side_));
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+    TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
+    launch_apply(RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    if (ovmode_ != 1) {
+        TRITD_HIP(hipEventRecord(evCtC_, st_));
+        TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
+        launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+        TRITD_HIP(hipEventRecord(evSA_, side_));
+    }
+    launch_k5_full(k);
+    phaseD(k);
 }
 
 void Session::phaseD(int k) {
@@ -295,13 +385,17 @@ void Session::run(int iters) {
             ev_iter_.push_back(k);
             TRITD_HIP(hipEventRecord(ev_[ev_.size() - 6], st_));
         }
-        phaseA(k);
-        allreduce(red1_.p, red1_count());
-        phaseB(k);
-        allreduce(red2_.p, red2_count());
-        phaseC(k);
-        allreduce(red3_.p, 2);
-        phaseD(k);
+        if (overlap_) {
+            iterate_overlapped(k);
+        } else {
+            phaseA(k);
+            allreduce(red1_.p, red1_count());
+            phaseB(k);
+            allreduce(red2_.p, red2_count());
+            phaseC(k);
+            allreduce(red3_.p, 2);
+            phaseD(k);
+        }
         if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 1], st_));
         maybe_print(k);
     }
@@ -325,6 +419,7 @@ void Session::harvest_timing() {
 
 void Session::sync(int* done, int* stopped) {
     TRITD_HIP(hipSetDevice(device_));
+    if (side_) TRITD_HIP(hipStreamSynchronize(side_));
     TRITD_HIP(hipStreamSynchronize(st_));
     if (!ev_.empty()) harvest_timing();
     int ctrl[3];

@@ -18,11 +18,12 @@ namespace tritd {
 struct DBuf {
     double* p = nullptr;
     size_t n = 0;
+    bool owned = true;  // false: a view into another DBuf
     DBuf() = default;
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() {
-        if (p) (void)hipFree(p);
+        if (p && owned) (void)hipFree(p);
     }
     void alloc(size_t count) {
         n = count;
@@ -77,6 +78,16 @@ class Session {
 
    private:
     void allreduce(double* buf, int64_t count);
+    // single-GPU schedule: the three R x R solves run on a side stream, each
+    // overlapped with the big kernel that precedes its consumer
+    void iterate_overlapped(int k);
+    void launch_k5_full(int k);
+    bool overlap_ = false;
+    int ovmode_ = 2;
+    hipStream_t side_ = nullptr;
+    hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
+    hipEvent_t evSA_ = nullptr, evSB_ = nullptr, evSC_ = nullptr;
+    DBuf GinvA_, GinvB_, GinvC_;
     void upload_factors(const double* A0, const double* B0, const double* C0);
     IterScalars scalars(int k) const;
 
@@ -90,6 +101,7 @@ class Session {
     double normD_ = 0.0;
     int k_enq_ = 0;
 
+    DBuf pool_;  // declared first: destroyed after the views into it
     DBuf D_, O_, E_, YL_, YO_, T_, Wk_;
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
     DBuf red1_, red2_, red3_;
