@@ -1,0 +1,138 @@
+// Mock mx runtime + a C entry point that drives mexFunction — TEST ONLY.
+#include "mex.h"
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <vector>
+
+struct mxArray {
+    mxClassID cls = mxDOUBLE_CLASS;
+    std::vector<mwSize> dims;
+    std::vector<double> data;
+    std::string str;
+    std::map<std::string, mxArray*> fields;
+};
+
+static std::string g_printed;
+
+bool mxIsStruct(const mxArray* a) { return a->cls == mxSTRUCT_CLASS; }
+bool mxIsDouble(const mxArray* a) { return a->cls == mxDOUBLE_CLASS; }
+bool mxIsComplex(const mxArray*) { return false; }
+bool mxIsChar(const mxArray* a) { return a->cls == mxCHAR_CLASS; }
+mxArray* mxGetField(const mxArray* a, size_t, const char* n) {
+    auto it = a->fields.find(n);
+    return it == a->fields.end() ? nullptr : it->second;
+}
+double mxGetScalar(const mxArray* a) { return a->data.empty() ? 0.0 : a->data[0]; }
+mwSize mxGetNumberOfDimensions(const mxArray* a) { return a->dims.size(); }
+const mwSize* mxGetDimensions(const mxArray* a) { return a->dims.data(); }
+size_t mxGetNumberOfElements(const mxArray* a) {
+    size_t n = 1;
+    for (auto d : a->dims) n *= d;
+    return n;
+}
+double* mxGetPr(const mxArray* a) { return const_cast<double*>(a->data.data()); }
+void mxSetM(mxArray* a, mwSize m) { a->dims[0] = m; }
+int mxGetString(const mxArray* a, char* buf, mwSize n) {
+    std::snprintf(buf, n, "%s", a->str.c_str());
+    return 0;
+}
+mxArray* mxCreateNumericArray(mwSize nd, const mwSize* d, mxClassID c, mxComplexity) {
+    auto* a = new mxArray;
+    a->cls = c;
+    a->dims.assign(d, d + nd);
+    a->data.assign(mxGetNumberOfElements(a), 0.0);
+    return a;
+}
+mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity c) {
+    const mwSize d[2] = {m, n};
+    return mxCreateNumericArray(2, d, mxDOUBLE_CLASS, c);
+}
+void mxDestroyArray(mxArray* a) {
+    for (auto& f : a->fields) mxDestroyArray(f.second);
+    delete a;
+}
+void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw MockMexError{id, buf};
+}
+int mexPrintf(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    const int n = std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_printed += buf;
+    return n;
+}
+
+static mxArray* dbl(const double* p, std::vector<mwSize> dims) {
+    mxArray* a = mxCreateNumericArray(dims.size(), dims.data(), mxDOUBLE_CLASS, mxREAL);
+    std::memcpy(a->data.data(), p, a->data.size() * sizeof(double));
+    return a;
+}
+
+extern "C" {
+// opt_names: comma-separated field names present in opts; opt_vals in the same order
+int mock_admm(const double* D, long n1, long n2, long n3, int r, const char* opt_names,
+              const double* opt_vals, const double* A0, const double* B0, const double* C0,
+              double* A, double* B, double* C, double* O, double* E, double* errHist, int* k,
+              char* err, int errlen, char* printed, int printlen) {
+    std::vector<mxArray*> in;
+    auto* cmd = new mxArray;
+    cmd->cls = mxCHAR_CLASS;
+    cmd->str = "admm";
+    cmd->dims = {1, 4};
+    in.push_back(cmd);
+    in.push_back(dbl(D, {(mwSize)n1, (mwSize)n2, (mwSize)n3}));
+    double rr = r;
+    in.push_back(dbl(&rr, {1, 1}));
+    auto* opts = new mxArray;
+    opts->cls = mxSTRUCT_CLASS;
+    opts->dims = {1, 1};
+    {
+        std::string names(opt_names);
+        size_t pos = 0;
+        int q = 0;
+        while (pos <= names.size() && !names.empty()) {
+            const size_t c = names.find(',', pos);
+            const std::string nm = names.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+            opts->fields[nm] = dbl(&opt_vals[q++], {1, 1});
+            if (c == std::string::npos) break;
+            pos = c + 1;
+        }
+    }
+    in.push_back(opts);
+    in.push_back(dbl(A0, {(mwSize)n1, (mwSize)r, (mwSize)r}));
+    in.push_back(dbl(B0, {(mwSize)r, (mwSize)n2, (mwSize)r}));
+    in.push_back(dbl(C0, {(mwSize)r, (mwSize)r, (mwSize)n3}));
+    mxArray* out[6] = {nullptr};
+    int rc = 0;
+    g_printed.clear();
+    try {
+        mexFunction(6, out, (int)in.size(), const_cast<const mxArray**>(in.data()));
+        const size_t nA = (size_t)n1 * r * r, nB = (size_t)r * n2 * r, nC = (size_t)r * r * n3;
+        const size_t N = (size_t)n1 * n2 * n3;
+        std::memcpy(A, out[0]->data.data(), nA * 8);
+        std::memcpy(B, out[1]->data.data(), nB * 8);
+        std::memcpy(C, out[2]->data.data(), nC * 8);
+        std::memcpy(O, out[3]->data.data(), N * 8);
+        *k = (int)out[4]->dims[0];
+        std::memcpy(errHist, out[4]->data.data(), (size_t)*k * 8);
+        std::memcpy(E, out[5]->data.data(), N * 8);
+    } catch (const MockMexError& e) {
+        std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
+        rc = 1;
+    }
+    std::snprintf(printed, printlen, "%s", g_printed.c_str());
+    for (auto* a : in) mxDestroyArray(a);
+    for (auto* a : out)
+        if (a) mxDestroyArray(a);
+    return rc;
+}
+}

@@ -1,0 +1,90 @@
+"""The MEX gateway (matlab/tritd_mex.cpp) compiled against a mock mx runtime
+(tests/mock_mex/) and driven through ctypes — MATLAB itself is absent
+(SURVEY.md §4.5).  CPU: argument parsing and MATLAB-style errors.  GPU: a
+full solve through the gateway matches the golden vectors."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG, ROOT, load_golden, rel
+
+MOCK = os.path.join(ROOT, "tests", "mock_mex")
+
+
+@pytest.fixture(scope="module")
+def gw(tmp_path_factory):
+    out = tmp_path_factory.mktemp("mex") / "libmexmock.so"
+    libdir = os.path.join(PKG, "tritd")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-shared", "-fPIC", "-I" + MOCK,
+                    "-I" + os.path.join(ROOT, "include"),
+                    os.path.join(PKG, "matlab", "tritd_mex.cpp"), os.path.join(MOCK, "mock_mex.cpp"),
+                    "-L" + libdir, "-ltritd", "-Wl,-rpath," + libdir, "-o", str(out)], check=True)
+    lib = C.CDLL(str(out))
+    lib.mock_admm.restype = C.c_int
+    return lib
+
+
+def run(gw, g, names=None, vals=None):
+    D = np.asfortranarray(g["D"])
+    n1, n2, n3 = D.shape
+    r = g["r"]
+    o = g["opts"]
+    names = names or ["mu", "rho", "lambda", "lambda2", "maxIter", "tol", "disp"]
+    vals = np.array(vals if vals is not None else [float(o[n]) for n in names])
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cc = np.zeros((r, r, n3), order="F")
+    O = np.zeros_like(D)
+    E = np.zeros_like(D)
+    eh = np.zeros(int(o["maxIter"]) + 1)
+    k = C.c_int(0)
+    err = C.create_string_buffer(1024)
+    pr = C.create_string_buffer(4096)
+    p = lambda a: C.c_void_p(a.ctypes.data)
+    A0, B0, C0 = (np.asfortranarray(g[x]) for x in ("A0", "B0", "C0"))
+    rc = gw.mock_admm(p(D), n1, n2, n3, r, ",".join(names).encode(), p(vals), p(A0), p(B0), p(C0),
+                      p(A), p(B), p(Cc), p(O), p(E), p(eh), C.byref(k), err, 1024, pr, 4096)
+    return rc, err.value.decode(), dict(A=A, B=B, C=Cc, O=O, E=E, errHist=eh[: k.value], k=k.value,
+                                        printed=pr.value.decode())
+
+
+def test_gateway_missing_field_error(gw):
+    g = load_golden("g12x10x8_r2")
+    names = ["mu", "rho", "lambda", "maxIter", "tol", "disp"]
+    rc, err, _ = run(gw, g, names, [float(g["opts"][n]) for n in names])
+    assert rc == 1
+    assert err == "MATLAB:nonExistentField|Reference to non-existent field 'lambda2'."
+
+
+def test_gateway_reports_missing_gpu(gw):
+    import tritd
+    if tritd.device_count() > 0:
+        pytest.skip("GPU visible")
+    rc, err, _ = run(gw, load_golden("g12x10x8_r2"))
+    assert rc == 1 and err.startswith("tritd:solver|") and "NODEV" not in err and "no HIP device" in err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["g30_r3", "g12x10x8_r2_stop", "g54x4x96_r5_sensor"])
+def test_gateway_solve_matches_golden(gw, name):
+    import tritd_oracle as orc
+    g = load_golden(name)
+    rc, err, res = run(gw, g)
+    assert rc == 0, err
+    assert res["k"] == g["k"]
+    assert rel(orc.triple_product(res["A"], res["B"], res["C"]),
+               orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
+    assert rel(res["O"], g["O"]) <= 1e-9 and rel(res["E"], g["E"]) <= 1e-9
+    np.testing.assert_allclose(res["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_gateway_disp_goes_through_mexPrintf(gw):
+    g = load_golden("g30_r3")
+    g["opts"] = dict(g["opts"], disp=1, maxIter=20)
+    rc, err, res = run(gw, g)
+    assert rc == 0, err
+    assert res["printed"].splitlines()[0].startswith("Iter 10, errL=")

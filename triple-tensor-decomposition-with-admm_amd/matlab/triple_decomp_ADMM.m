@@ -1,0 +1,16 @@
+function [A, B, C, O, errHist, E] = triple_decomp_ADMM(D, r, opts)
+%TRIPLE_DECOMP_ADMM  MI355X drop-in for fast_robust_triple_tensor/triple_decomp_ADMM.m.
+%   [A,B,C,O,errHist] = triple_decomp_ADMM(D, r, opts) runs the robust
+%   triple-decomposition ADMM on the GPU (libtritd.so via tritd_mex) with the
+%   reference's inputs, outputs, opts fields and stopping rule.  A sixth
+%   output E (the sparse copy) is available; the reference never returns it.
+%
+%   The initial factors are drawn here with randn in the reference's order
+%   (A, then B, then C), so the global RNG stream and the starting point are
+%   those of the reference run.  D is processed in double precision.
+[n1, n2, n3] = size(D);
+A0 = randn(n1, r, r);
+B0 = randn(r, n2, r);
+C0 = randn(r, r, n3);
+[A, B, C, O, errHist, E] = tritd_mex('admm', double(D), r, opts, A0, B0, C0);
+end
