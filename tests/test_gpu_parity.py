@@ -3,7 +3,7 @@
 Tolerances (fp64; BASELINE.json north_star "within a stated fp64 tolerance"):
   * L = triple_product(A,B,C), O, E : relative Frobenius <= 1e-9
   * A, B, C                         : relative Frobenius <= 1e-8
-  * errHist                         : |d| <= 1e-8*errHist + 1e-13 entrywise, same k
+  * errHist                         : |d| <= 1e-8*errHist + 1e-11 entrywise, same k
     (errHist is ||resL||/||D|| + ||resO||/||D||; resL = D - L - O cancels, so
     its rounding floor is ~eps in units of ||D||, hence the absolute floor)
   * data-movement primitives (unfold, buildF/G/H, soft_threshold): bit-exact
@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 TOL_LOE = 1e-9
 TOL_ABC = 1e-8
 TOL_ERR = 1e-8
-ATOL_ERR = 1e-13
+ATOL_ERR = 1e-11
 
 
 @pytest.fixture(scope="module")
