@@ -157,11 +157,11 @@ def main():
     errhist_final = float(res["errHist"][-1]) if len(res["errHist"]) else None
 
     # algorithmic bytes of the dominant kernel (fused update K5), per launch,
-    # on this rank's shard: reads D,Y_L,E,Y_O + writes O,E,Y_L,Y_O,T (9 N-streams)
-    # + W (R * n1 * n2 doubles); SURVEY.md §8d / DESIGN.md §4
+    # on this rank's shard: reads D,Y_L,E,Y_O + writes E,Y_L,Y_O,T (8 N-streams;
+    # O is rebuilt on demand) + W (R * n1 * n2 doubles)
     nl = i1 - i0
     N_local = nl * n * n
-    k5_bytes = (9 * N_local + r * r * nl * n) * 8
+    k5_bytes = (8 * N_local + r * r * nl * n) * 8
     k5_ms = km["fused_update"]
     achieved = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
     traffic, traffic_src = pmc_traffic()

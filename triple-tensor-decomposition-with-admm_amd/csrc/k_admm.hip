@@ -8,8 +8,11 @@
 //   ||resL||^2, ||resO||^2                       :59
 //   T_next = D - O + (1/muL_next)*Y_L            :33 of the NEXT iteration
 //   W(ij,k) = sum_t T_next(ij,t) C^(t,k)         mode-1/2 half of update_A/update_B (:78,:86)
-// in one pass: reads D, Y_L, E, Y_O and writes O, E, Y_L, Y_O, T (9 N-streams)
-// plus W (N*R/n3 elements).
+// in one pass: reads D, Y_L, E, Y_O and writes E, Y_L, Y_O, T (8 N-streams)
+// plus W (N*R/n3 elements).  O is never read inside the loop (E, not O, feeds
+// :42), so it is not stored: T_{k+1} = (D - O_k) + Y_L/muL_{k+1} determines it
+// and k_o_fixup rebuilds O_k = (D + Y_L/muL_{k+1}) - T_{k+1} when the caller
+// asks for it (relative error ~1e-16).
 //
 // Work decomposition: a wave owns one ij-tile (16 consecutive rows i of one
 // fibre j) and walks all its t-tiles of 16.  The big tensors are tile-major
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
             for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                d2v On2, En2, YLn2, YOn2;
+                d2v En2, YLn2, YOn2;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int r = 2 * p + q;
@@ -179,14 +182,12 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
                     const double Tn = (d - On) + sc.invL_next * YLn;        // :33 (k+1)
                     ssL += rL * rL;
                     ssO += rO * rO;
-                    On2[q] = On;
                     En2[q] = En;
                     YLn2[q] = YLn;
                     YOn2[q] = YOn;
                     tr[r] = Tn;
                 }
                 if (active) {
-                    O2[o + 64 * p] = On2;
                     E2[o + 64 * p] = En2;
                     YL2[o + 64 * p] = YLn2;
                     YO2[o + 64 * p] = YOn2;
@@ -325,6 +326,31 @@ void launch_finish(const double* ss, double normD, int k, double tol, double* er
                    double* errO, int* ctrl, hipStream_t st) {
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, ss, normD, k, tol, errHist, errL, errO,
                        ctrl);
+    TRITD_CHECK_LAUNCH();
+}
+
+// O_k = (D + (1/muL_{k+1}) Y_L) - T_{k+1}: D, Y_L, O in tile-major order,
+// T in the TX order of the same tile (common.h)
+__global__ __launch_bounds__(256) void k_o_fixup(const double* __restrict__ D,
+                                                 const double* __restrict__ YL,
+                                                 const double* __restrict__ T, double invL_next,
+                                                 double* __restrict__ O, int64_t Np) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < Np; e += (int64_t)gridDim.x * 256) {
+        const int w = (int)(e & 255);
+        const int p = w >> 7, l = (w & 127) >> 1, q = w & 1;
+        const int r = 2 * p + q;
+        const int il = l & 15, tl = (l >> 4) + 4 * r;  // element of this TM slot
+        const int s = il >> 2, lx = ((il & 3) << 4) | tl;  // its TX slot
+        const int64_t tx = (e & ~(int64_t)255) + ((s >> 1) << 7) + (lx << 1) + (s & 1);
+        O[e] = (D[e] + invL_next * YL[e]) - T[tx];
+    }
+}
+
+void launch_o_fixup(const Geom& g, const double* D, const double* YL, const double* T,
+                    double invL_next, double* O, hipStream_t st) {
+    int64_t b = cdiv(g.Np, 256);
+    if (b > 16384) b = 16384;
+    hipLaunchKernelGGL(k_o_fixup, dim3((unsigned)b), dim3(256), 0, st, D, YL, T, invL_next, O, g.Np);
     TRITD_CHECK_LAUNCH();
 }
 

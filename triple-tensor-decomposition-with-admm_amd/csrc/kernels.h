@@ -30,6 +30,9 @@ struct K5Args {
 };
 int k5_grid(const Geom& g);
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st);
+// O_k = (D + invL_next*Y_L) - T_{k+1} (O is not stored by K5)
+void launch_o_fixup(const Geom& g, const double* D, const double* YL, const double* T,
+                    double invL_next, double* O, hipStream_t st);
 // partial sums -> out[0..1] (fixed-order tree)
 void launch_reduce_pairs(const double* partial, int n, double* out, const int* stop, hipStream_t st);
 // errHist bookkeeping + stop test (triple_decomp_ADMM.m:59,63)

@@ -461,6 +461,8 @@ void Session::get(double* A, double* B, double* C, double* O, double* E, int64_t
         TRITD_HIP(hipMemcpy(h.data(), Ch_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
         unpack_C(g_, h, C);
     }
+    if (O && g_.n1l > 0 && done > 0)  // O of iteration `done` from D, Y_L, T (K5 does not store it)
+        launch_o_fixup(g_, D_.p, YL_.p, T_.p, 1.0 / mu_[(size_t)done], O_.p, st_);
     if ((O || E) && g_.n1l > 0) {
         DBuf tmp;
         tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));
