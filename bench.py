@@ -136,6 +136,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     km = sess.kernel_ms()
+    probe_ms, probe_pick = sess.probe()
     if dist is not None:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -200,6 +201,9 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": k5_bytes},
             "cpu_baseline": cpu,
+            # candidate tensor pools timed with K5's access pattern at session
+            # creation (rank 0), the fastest kept
+            "placement_probe": {"ms": [round(m, 4) for m in probe_ms], "picked": probe_pick},
         }
         print(json.dumps(line), flush=True)
 

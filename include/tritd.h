@@ -137,6 +137,11 @@ tritd_status tritd_session_rre_parts(tritd_session* s, const double* dX, int64_t
 tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable);
 tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, double* mode3_ms,
                                      double* iteration_ms, int32_t* samples);
+/* Placement probe of the session's tensor pool: the probe
+ * time (ms) of each candidate pool that was tried (up to cap entries) and
+ * the index kept.  *n = 1 when probing was skipped. */
+tritd_status tritd_session_probe(tritd_session* s, double* ms, int32_t cap, int32_t* n,
+                                 int32_t* picked);
 void tritd_session_destroy(tritd_session* s);
 
 /* ---------------------------------------------------------------------------

@@ -140,3 +140,24 @@ def test_config4_recovers_low_rank(tritd, big):
     assert k == 60 and not stopped
     assert np.sqrt(num / den) < 1e-6
     assert res["errHist"][-1] < 1e-3 * res["errHist"][0]
+
+
+def test_config4_pool_probe_does_not_change_results(tritd, big, monkeypatch):
+    """Placement probing picks one of several candidate pools; addresses never
+    enter the arithmetic, so every choice gives bitwise the same iterates."""
+    from tritd import synth
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
+    n = 512
+    out = []
+    for probe in ("1", "3"):
+        monkeypatch.setenv("TRITD_PROBE", probe)
+        s = tritd.Session(8, opts, big["A0"], big["B0"], big["C0"], n1=n, n2=n, n3=n,
+                          D=big["D"], device=0)
+        ms, picked = s.probe()
+        assert len(ms) == int(probe) and 0 <= picked < len(ms)
+        assert all(m > 0 for m in ms) if len(ms) > 1 else True
+        s.run(3)
+        out.append(s.get())
+        s.close()
+    for key in ("A", "B", "C", "O", "E", "errHist"):
+        np.testing.assert_array_equal(out[0][key], out[1][key])

@@ -1,0 +1,28 @@
+"""Dev helper: interleaved in-process A/B of an env knob read at session creation.
+usage: python tools/ab_env.py VAR v1,v2[,..] reps [iters]"""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd"))
+import numpy as np
+import tritd
+from tritd import synth
+var, vals, reps = sys.argv[1], sys.argv[2].split(","), int(sys.argv[3])
+iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+n, r = 512, 8
+rng = np.random.default_rng(0)
+D = np.asfortranarray(rng.standard_normal((n, n, n)))
+A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
+opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
+res = {v: [] for v in vals}
+for rep in range(reps):
+    for v in vals:
+        os.environ[var] = v
+        s = tritd.Session(r, opts, A0, B0, C0, n1=n, n2=n, n3=n, D=D, device=0)
+        s.run(2); s.sync(); s.set_timing(True); s.run(iters); s.sync()
+        km = s.kernel_ms()
+        res[v].append((km["iteration"], km["fused_update"], km["mode3"]))
+        print("%s=%s rep %d: it %.3f k5 %.3f m3 %.3f" % (var, v, rep, km["iteration"], km["fused_update"], km["mode3"]), flush=True)
+        s.close()
+for v in vals:
+    a = np.array(res[v])
+    print("%s=%s median it %.3f k5 %.3f m3 %.3f | min it %.3f" % (var, v, *np.median(a, 0), a[:, 0].min()))

@@ -1,0 +1,38 @@
+"""Dev helper: interleaved in-process A/B of two (or more) builds of libtritd.so.
+usage: python tools/ab_lib.py lib1.so,lib2.so reps [iters]"""
+import ctypes as C
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd"))
+import numpy as np
+import tritd
+from tritd import _lib, api, synth
+paths, reps = sys.argv[1].split(","), int(sys.argv[2])
+iters = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+libs = {}
+for p in paths:
+    l = C.CDLL(os.path.abspath(p))
+    for name, (res, args) in _lib.SIGNATURES.items():
+        if not hasattr(l, name):
+            continue
+        fn = getattr(l, name); fn.restype = res; fn.argtypes = args
+    libs[p] = l
+n, r = 512, 8
+rng = np.random.default_rng(0)
+D = np.asfortranarray(rng.standard_normal((n, n, n)))
+A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
+opts = dict(synth.TRAFFIC_OPTS, maxIter=100, tol=float(os.environ.get("AB_TOL", "1e-5")))
+res = {p: [] for p in paths}
+for rep in range(reps):
+    for p in paths:
+        api.lib = _lib.lib = libs[p]
+        s = tritd.Session(r, opts, A0, B0, C0, n1=n, n2=n, n3=n, D=D, device=0)
+        s.run(2); s.sync(); s.set_timing(True); s.run(iters); s.sync()
+        km = s.kernel_ms()
+        pr = s.probe() if hasattr(libs[p], "tritd_session_probe") else None
+        res[p].append((km["iteration"], km["fused_update"], km["mode3"]))
+        print("%s rep %d: it %.3f k5 %.3f m3 %.3f probe %s" % (p, rep, km["iteration"], km["fused_update"], km["mode3"], pr), flush=True)
+        s.close()
+for p in paths:
+    a = np.array(res[p])
+    print("%s median it %.3f k5 %.3f m3 %.3f | min it %.3f" % (p, *np.median(a, 0), a[:, 0].min()))

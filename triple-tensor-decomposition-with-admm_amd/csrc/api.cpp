@@ -209,6 +209,18 @@ tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, 
     });
 }
 
+tritd_status tritd_session_probe(tritd_session* s, double* ms, int32_t cap, int32_t* n,
+                                 int32_t* picked) {
+    return guarded([&] {
+        need(s, "session");
+        const Session* q = reinterpret_cast<Session*>(s);
+        const std::vector<double>& v = q->probe_ms();
+        for (int32_t c = 0; ms && c < cap && c < (int32_t)v.size(); ++c) ms[c] = v[c];
+        if (n) *n = (int32_t)v.size();
+        if (picked) *picked = q->probe_pick();
+    });
+}
+
 void tritd_session_destroy(tritd_session* s) { delete reinterpret_cast<Session*>(s); }
 
 tritd_status tritd_comm_unique_id(void* id128) {

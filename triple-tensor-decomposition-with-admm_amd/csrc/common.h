@@ -40,7 +40,10 @@ inline bool rp_supported(int RP) { return RP == 16 || RP == 32 || RP == 48 || RP
 // Geometry of one shard in the device layout:
 //   big tensors (D, O, E, Y_L, Y_O, T) are TILE-MAJOR ("TM"):
 //     ij-tile g = (j*n1p + i)/16 (16 consecutive rows i of one fibre j),
-//     t-tile tt = t/16; tile (g, tt) = 256 contiguous doubles at (g*ntt + tt)*256.
+//     t-tile tt = t/16; tile (g, tt) = 256 contiguous doubles, and the 4
+//     ij-tiles of a group g/4 (the 4 waves of one K5 workgroup) are
+//     interleaved per t-tile: tile (g, tt) at ((g/4*ntt + tt)*4 + g%4)*256, so
+//     a workgroup reads or writes 8 KB contiguous per tensor per t-tile.
 //     Inside a tile, element (r, l) of the f64 MFMA C/D fragment
 //     (t%16 = (l>>4) + 4r, i%16 = l&15) sits at (r>>1)*128 + 2l + (r&1), so a
 //     wave reads/writes a tile as two fully contiguous 1 KB dwordx4 sweeps and
@@ -62,6 +65,8 @@ struct Geom {
     int64_t Np = 0;                  // plane * n3p
     int64_t tiles = 0;               // plane / 16 (ij-tiles of 16 rows)
     int64_t ntt = 0;                 // n3p / 16 (t-tiles)
+    int64_t tiles4 = 0;              // tiles rounded up to the group of 4
+    int64_t Ntm = 0;                 // doubles of one tile-major tensor (tiles4*ntt*256)
 };
 
 inline Geom make_geom(int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1, int r) {
@@ -74,6 +79,8 @@ inline Geom make_geom(int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1
     g.Np = g.plane * g.n3p;
     g.tiles = g.plane / 16;
     g.ntt = g.n3p / 16;
+    g.tiles4 = round_up(g.tiles, 4);
+    g.Ntm = g.tiles4 * g.ntt * 256;
     return g;
 }
 
@@ -88,12 +95,17 @@ struct IterScalars {
     double invL_next;    // 1/muL of the next iteration (fused T formation, :33)
 };
 
+// first double of tile (g, tt) in the tile-major layout
+__host__ __device__ inline int64_t tm_tile_base(int64_t g, int64_t tt, int64_t ntt) {
+    return ((((g >> 2) * ntt + tt) << 2) + (g & 3)) << 8;
+}
+
 // TM offset of element (i, j, t) of a shard (i < n1p, t < n3p)
 __host__ __device__ inline int64_t tm_offset(int64_t i, int64_t j, int64_t t, int64_t n1p, int64_t ntt) {
     const int64_t g = (j * n1p + i) >> 4;
     const int il = (int)(i & 15), tl = (int)(t & 15);
     const int r = tl >> 2, l = ((tl & 3) << 4) | il;
-    return ((g * ntt + (t >> 4)) << 8) + ((r >> 1) << 7) + (l << 1) + (r & 1);
+    return tm_tile_base(g, t >> 4, ntt) + ((r >> 1) << 7) + (l << 1) + (r & 1);
 }
 
 }  // namespace tritd

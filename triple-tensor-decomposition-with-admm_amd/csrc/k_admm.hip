@@ -35,10 +35,18 @@ namespace tritd {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 static constexpr int K5_WAVES = 4;
+#ifndef K5_NT
+#define K5_NT 0  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores
+#endif
+#ifndef K5_EXP
+#define K5_EXP 0  // timing experiments only (tools/): drop parts of the t-tile work
+#endif
 
 __device__ __forceinline__ double matlab_sign(double x) {
-    // sign(): 1 / -1 / 0, NaN stays NaN
-    return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x));
+    // sign(): 1 / -1 / 0 (also for -0), NaN stays NaN; selects only, no
+    // branches (a divergent branch would break the K5 loop's exact vmcnt waits)
+    const double s = x == 0.0 ? 0.0 : __builtin_copysign(1.0, x);
+    return __builtin_isnan(x) ? x : s;
 }
 
 __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
@@ -46,6 +54,17 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
 }
 
 typedef double d2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ d2v ld2(const d2v* p) {
+    if (K5_NT & 1) return __builtin_nontemporal_load(p);
+    return *p;
+}
+__device__ __forceinline__ void st2(d2v v, d2v* p) {
+    if (K5_NT & 2)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
 
 template <int RP, bool PRO>
 __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
@@ -63,9 +82,7 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     const int64_t j = active ? tile / qper : 0;
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
-    // this lane's d2v slots inside the wave's stream: tile tt, pair p at
-    // stream + tt*128 + p*64 + lane   (in units of d2v)
-    const int64_t sbase = tile * ntt * 128 + lane;
+    // this lane's d2v slot of pair p in t-tile tt: tm_tile_base(tile, tt)/2 + 64p + lane
 
     // C^ rows of one t-tile, staged once per workgroup (double buffered):
     //   sCT[k][16]  (L operand: C^(t0+l&15, 4s+(l>>4)))
@@ -75,17 +92,42 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
     __shared__ double tsm[K5_WAVES][16 * 17];
     double* ts = tsm[wid];
-    auto stage = [&](int64_t tt, int buf) {
-        // 16 rows x RP of Ch (row-major [t][RP]), 2 doubles per thread-step
-        for (int e = threadIdx.x; e < 16 * RP / 2; e += 64 * K5_WAVES) {
-            const int row = (2 * e) / RP, k = (2 * e) % RP;
-            const double* src = a.Ch + ((tt << 4) + row) * RP + k;
-            const double v0 = src[0], v1 = src[1];
-            sC[buf][row * LDC + k] = v0;
-            sC[buf][row * LDC + k + 1] = v1;
-            sCT[buf][k * 16 + row] = v0;
-            sCT[buf][(k + 1) * 16 + row] = v1;
+    // Rotated t-walk: resident workgroups start at different t-tiles so that
+    // their concurrent streams do not advance in lockstep 64 KB apart (HBM
+    // channel hot-spotting).  Any fixed order is deterministic.
+    const int64_t rot = a.rot ? ((int64_t)blockIdx.x * 7) % ntt : 0;
+    auto phys = [&](int64_t tt) { int64_t x = tt + rot; return x >= ntt ? x - ntt : x; };
+    // Staging is split so that its global loads are issued before the tile
+    // prefetch and its LDS writes come after this t-tile's compute: vmcnt is
+    // in-order, so a wait on a load issued after the prefetch would also wait
+    // for the prefetch (measured: the prefetch was serialized every t-tile).
+    constexpr int SP = 16 * RP / 2;                 // (v0,v1) pairs per slice
+    constexpr int NS = (SP + 64 * K5_WAVES - 1) / (64 * K5_WAVES);
+    d2v sv[NS];
+    auto stage_load = [&](int64_t tt) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 64 * K5_WAVES;
+            if (SP % (64 * K5_WAVES) == 0 || e < SP)
+                sv[q] = *reinterpret_cast<const d2v*>(a.Ch + (phys(tt) << 4) * RP + 2 * e);
         }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 64 * K5_WAVES;
+            if (SP % (64 * K5_WAVES) == 0 || e < SP) {
+                const int row = (2 * e) / RP, k = (2 * e) % RP;
+                sC[buf][row * LDC + k] = sv[q][0];
+                sC[buf][row * LDC + k + 1] = sv[q][1];
+                sCT[buf][k * 16 + row] = sv[q][0];
+                sCT[buf][(k + 1) * 16 + row] = sv[q][1];
+            }
+        }
+    };
+    auto stage = [&](int64_t tt, int buf) {
+        stage_load(tt);
+        stage_store(buf);
     };
 
     double kr[KS];
@@ -109,41 +151,38 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     d2v* YO2 = reinterpret_cast<d2v*>(a.YO);
     d2v* T2 = reinterpret_cast<d2v*>(a.T);
 
-    // register double buffer: [0] = D, [1] = Y_L, [2] = E (PRO: O), [3] = Y_O
-    d2v nx[4][2];
-    auto load = [&](int64_t tt) {
-        if (!active) return;
-        const int64_t o = sbase + tt * 128;
+    // Two register sets [0] = D, [1] = Y_L, [2] = E (PRO: O), [3] = Y_O.  The
+    // t-walk is unrolled by two so that the sets alternate by name: a copy
+    // cur = next would make the compiler wait for the prefetch at the copy.
+    // Inside the walk nothing depends on `active` (a wave past the last tile
+    // streams the zero-filled group padding, see common.h), so the
+    // steady-state loop has no control-flow joins and the in-order vmcnt
+    // waits stay exact.
+    auto load = [&](int64_t tt, d2v (&nx)[4][2]) {
+        const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            nx[0][p] = D2[o + 64 * p];
-            nx[1][p] = YL2[o + 64 * p];
+            nx[0][p] = ld2(D2 + o + 64 * p);
+            nx[1][p] = ld2(YL2 + o + 64 * p);
             if (PRO) {
-                nx[2][p] = O2[o + 64 * p];
+                nx[2][p] = ld2(O2 + o + 64 * p);
             } else {
-                nx[2][p] = E2[o + 64 * p];
-                nx[3][p] = YO2[o + 64 * p];
+                nx[2][p] = ld2(E2 + o + 64 * p);
+                nx[3][p] = ld2(YO2 + o + 64 * p);
             }
         }
     };
-#pragma unroll
-    for (int q = 0; q < 4; ++q) nx[q][0] = nx[q][1] = d2v{0.0, 0.0};
-    load(0);
-    stage(0, 0);
-    __syncthreads();
-    for (int64_t tt = 0; tt < ntt; ++tt) {
-        const int buf = (int)(tt & 1);
-        d2v cx[4][2];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            cx[q][0] = nx[q][0];
-            cx[q][1] = nx[q][1];
+    // one t-tile: cx holds its data; if `pf`, tile tt+1 is prefetched into nx
+    // and its C^ slice staged into buffer buf^1
+    auto body = [&](int64_t tt, int buf, d2v (&cx)[4][2], d2v (&nx)[4][2], bool pf) {
+        if (pf) {
+            stage_load(tt + 1);
+            load(tt + 1, nx);
+            // keep the prefetch at the top: the scheduler otherwise sinks it
+            // next to the stores (less register pressure, no latency hiding)
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (tt + 1 < ntt) {
-            load(tt + 1);
-            stage(tt + 1, buf ^ 1);
-        }
-        const int64_t o = sbase + tt * 128;
+        const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
         const double* cT = sCT[buf];
         const double* cR = sC[buf];
         double tr[4];
@@ -159,8 +198,9 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
             }
         } else {
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
+            if (!(K5_EXP & 1))
 #pragma unroll
-            for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
+                for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 d2v En2, YLn2, YOn2;
@@ -187,35 +227,59 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
                     YOn2[q] = YOn;
                     tr[r] = Tn;
                 }
-                if (active) {
-                    E2[o + 64 * p] = En2;
-                    YL2[o + 64 * p] = YLn2;
-                    YO2[o + 64 * p] = YOn2;
-                }
+                st2(En2, E2 + o + 64 * p);
+                st2(YLn2, YL2 + o + 64 * p);
+                st2(YOn2, YO2 + o + 64 * p);
             }
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
+        if (K5_EXP & 8) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) st2(d2v{tr[2 * p], tr[2 * p + 1]}, T2 + o + 64 * p);
+        } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ts[(tg + 4 * r) * 17 + il] = tr[r];
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (active) {
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                d2v tv;
-                tv[0] = ts[il * 17 + 4 * (2 * p) + tg];
-                tv[1] = ts[il * 17 + 4 * (2 * p + 1) + tg];
-                T2[o + 64 * p] = tv;
-            }
+        for (int p = 0; p < 2; ++p) {
+            d2v tv;
+            tv[0] = ts[il * 17 + 4 * (2 * p) + tg];
+            tv[1] = ts[il * 17 + 4 * (2 * p + 1) + tg];
+            st2(tv, T2 + o + 64 * p);
+        }
         }
         // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+            if (!(K5_EXP & 2)) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
                 wacc[m] = mfma4(cR[(4 * r + tg) * LDC + 16 * m + il], tr[r], wacc[m]);
+            } else {
+                for (int m = 0; m < MT; ++m) wacc[m][0] += tr[r];
+            }
         }
-        __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
+        if (pf) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
+        if (!(K5_EXP & 4)) __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
+    };
+
+    d2v xa[4][2], xb[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xa[q][0] = xa[q][1] = xb[q][0] = xb[q][1] = d2v{0.0, 0.0};
+    load(0, xa);
+    stage(0, 0);
+    __syncthreads();
+    int64_t tt = 0;
+    for (; tt + 2 < ntt; tt += 2) {
+        body(tt, 0, xa, xb, true);
+        body(tt + 1, 1, xb, xa, true);
+    }
+    if (tt + 1 < ntt) {
+        body(tt, 0, xa, xb, true);
+        body(tt + 1, 1, xb, xa, false);
+    } else {
+        body(tt, 0, xa, xb, false);
     }
     if (active) {
         // W^T C/D layout: row k = 16m + tg + 4rr, col ij = il
@@ -309,9 +373,8 @@ void launch_reduce_pairs(const double* partial, int n, double* out, const int* s
 }
 
 // ctrl[0] = stop flag, ctrl[1] = iterations completed (k of :68)
-__global__ void k_finish(const double* ss, double normD, int k, double tol, double* errHist,
-                         double* errL, double* errO, int* ctrl) {
-    if (ctrl[0]) return;
+__device__ __forceinline__ void finish_body(const double* ss, double normD, int k, double tol,
+                                            double* errHist, double* errL, double* errO, int* ctrl) {
     const double eL = sqrt(ss[0]) / normD;  // norm(resL(:))/normD
     const double eO = sqrt(ss[1]) / normD;  // norm(resO(:))/normD
     const double e = eL + eO;               // :59
@@ -320,6 +383,46 @@ __global__ void k_finish(const double* ss, double normD, int k, double tol, doub
     errO[k - 1] = eO;
     ctrl[1] = k;
     if (k > 1 && fabs(e - errHist[k - 2]) < tol * errHist[k - 2]) ctrl[0] = 1;  // :63
+}
+
+__global__ void k_finish(const double* ss, double normD, int k, double tol, double* errHist,
+                         double* errL, double* errO, int* ctrl) {
+    if (ctrl[0]) return;
+    finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl);
+}
+
+__global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict__ p, int n,
+                                                       double normD, int k, double tol,
+                                                       double* errHist, double* errL, double* errO,
+                                                       int* ctrl) {
+    if (ctrl[0]) return;
+    __shared__ double sx[256], sy[256];
+    double x = 0.0, y = 0.0;
+    for (int b = threadIdx.x; b < n; b += 256) {
+        x += p[2 * b];
+        y += p[2 * b + 1];
+    }
+    sx[threadIdx.x] = x;
+    sy[threadIdx.x] = y;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            sx[threadIdx.x] += sx[threadIdx.x + w];
+            sy[threadIdx.x] += sy[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double ss[2] = {sx[0], sy[0]};
+        finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl);
+    }
+}
+
+void launch_reduce_finish(const double* partial, int n, double normD, int k, double tol,
+                          double* errHist, double* errL, double* errO, int* ctrl, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce_finish, dim3(1), dim3(256), 0, st, partial, n, normD, k, tol,
+                       errHist, errL, errO, ctrl);
+    TRITD_CHECK_LAUNCH();
 }
 
 void launch_finish(const double* ss, double normD, int k, double tol, double* errHist, double* errL,
@@ -348,9 +451,66 @@ __global__ __launch_bounds__(256) void k_o_fixup(const double* __restrict__ D,
 
 void launch_o_fixup(const Geom& g, const double* D, const double* YL, const double* T,
                     double invL_next, double* O, hipStream_t st) {
-    int64_t b = cdiv(g.Np, 256);
+    int64_t b = cdiv(g.Ntm, 256);
     if (b > 16384) b = 16384;
-    hipLaunchKernelGGL(k_o_fixup, dim3((unsigned)b), dim3(256), 0, st, D, YL, T, invL_next, O, g.Np);
+    hipLaunchKernelGGL(k_o_fixup, dim3((unsigned)b), dim3(256), 0, st, D, YL, T, invL_next, O, g.Ntm);
+    TRITD_CHECK_LAUNCH();
+}
+
+// Placement probe: K5's exact HBM pattern (read D, Y_L, E, Y_O; write E, Y_L,
+// Y_O in place and T; one wave per ij-tile walking its t-tiles, prefetched)
+// without the arithmetic.  K5 is HBM-bound (dropping all its compute leaves
+// its time unchanged) and its bandwidth depends on where the pool landed
+// physically; the session times candidate pools with this and keeps the
+// fastest.  Contents are overwritten with garbage.
+__global__ __launch_bounds__(256) void k_pool_probe(double* D, double* E, double* YL, double* YO,
+                                                    double* T, int64_t tiles4, int64_t ntt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= tiles4) return;
+    d2v* P[5] = {reinterpret_cast<d2v*>(D), reinterpret_cast<d2v*>(YL), reinterpret_cast<d2v*>(E),
+                 reinterpret_cast<d2v*>(YO), reinterpret_cast<d2v*>(T)};
+    auto off = [&](int64_t tt) { return (tm_tile_base(tile, tt, ntt) >> 1) + lane; };
+    d2v xa[4][2], xb[4][2];
+    auto load = [&](int64_t tt, d2v (&nx)[4][2]) {
+        const int64_t o = off(tt);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) nx[f][p] = P[f][o + 64 * p];
+    };
+    auto body = [&](int64_t tt, d2v (&c)[4][2], d2v (&n)[4][2], bool pf) {
+        if (pf) {
+            load(tt + 1, n);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const int64_t o = off(tt);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            P[1][o + 64 * p] = c[0][p] + c[1][p];
+            P[2][o + 64 * p] = c[2][p] - c[3][p];
+            P[3][o + 64 * p] = c[1][p] - c[3][p];
+            P[4][o + 64 * p] = c[0][p] - c[2][p];
+        }
+    };
+    load(0, xa);
+    int64_t tt = 0;
+    for (; tt + 2 < ntt; tt += 2) {
+        body(tt, xa, xb, true);
+        body(tt + 1, xb, xa, true);
+    }
+    if (tt + 1 < ntt) {
+        body(tt, xa, xb, true);
+        body(tt + 1, xb, xa, false);
+    } else {
+        body(tt, xa, xb, false);
+    }
+}
+
+void launch_pool_probe(const Geom& g, double* D, double* E, double* YL, double* YO, double* T,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_pool_probe, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D, E, YL, YO,
+                       T, g.tiles4, g.ntt);
     TRITD_CHECK_LAUNCH();
 }
 

@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
             const int64_t tt = tb * 4 + n;
 #pragma unroll
             for (int p = 0; p < 2; ++p)
-                nb[n][p] = (tt < ntt) ? T2[(g * ntt + tt) * 128 + 64 * p + lane] : d2v{0.0, 0.0};
+                nb[n][p] = (tt < ntt) ? __builtin_nontemporal_load(T2 + (tm_tile_base(g, tt, ntt) >> 1) + 64 * p + lane)
+                                      : d2v{0.0, 0.0};
         }
     };
     if (g0 < g1) loadB(g0);

@@ -31,13 +31,13 @@ __global__ __launch_bounds__(256) void k_sumsq(const double* __restrict__ X, int
 }
 
 int sumsq_blocks(const Geom& g) {
-    int64_t b = cdiv(g.Np, 256 * 8);
+    int64_t b = cdiv(g.Ntm, 256 * 8);
     return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048);
 }
 
 void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nblocks,
                          hipStream_t st) {
-    hipLaunchKernelGGL(k_sumsq, dim3(nblocks), dim3(256), 0, st, X, g.Np, partial);
+    hipLaunchKernelGGL(k_sumsq, dim3(nblocks), dim3(256), 0, st, X, g.Ntm, partial);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -287,15 +287,16 @@ __global__ __launch_bounds__(256) void k_to_tm(const double* __restrict__ src, i
                                                int64_t n1l, int64_t n2, int64_t n3, int64_t n1p,
                                                int64_t ntt, int64_t Np, double* __restrict__ dst) {
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < Np; e += (int64_t)gridDim.x * 256) {
-        const int64_t tile = e >> 8;
-        const int64_t g = tile / ntt, tt = tile - g * ntt;
+        const int64_t blk = e >> 8;  // ((g/4)*ntt + tt)*4 + g%4
+        const int64_t q4 = blk >> 2, grp = q4 / ntt, tt = q4 - grp * ntt;
+        const int64_t g = grp * 4 + (blk & 3);
         const int w = (int)(e & 255);
         const int p = w >> 7, l = (w & 127) >> 1, q = w & 1;
         const int r = 2 * p + q;
         const int64_t t = 16 * tt + (l >> 4) + 4 * r;
         const int64_t row = 16 * g + (l & 15);
         const int64_t j = row / n1p, i = row - j * n1p;
-        dst[e] = (i < n1l && t < n3) ? src[(t * n2 + j) * ld + i] : 0.0;
+        dst[e] = (i < n1l && j < n2 && t < n3) ? src[(t * n2 + j) * ld + i] : 0.0;
     }
 }
 
@@ -317,8 +318,8 @@ static unsigned grid_for(int64_t n) {
 }
 
 void launch_to_tm(const Geom& g, const double* src, int64_t ld, double* dst, hipStream_t st) {
-    hipLaunchKernelGGL(k_to_tm, dim3(grid_for(g.Np)), dim3(256), 0, st, src, ld, g.n1l, g.n2, g.n3,
-                       g.n1p, g.ntt, g.Np, dst);
+    hipLaunchKernelGGL(k_to_tm, dim3(grid_for(g.Ntm)), dim3(256), 0, st, src, ld, g.n1l, g.n2, g.n3,
+                       g.n1p, g.ntt, g.Ntm, dst);
     TRITD_CHECK_LAUNCH();
 }
 

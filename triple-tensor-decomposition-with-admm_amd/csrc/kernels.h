@@ -27,14 +27,20 @@ struct K5Args {
     int64_t n1p, n2, n3p, plane, tiles, ntt;
     IterScalars s;
     const int* stop;
+    int rot;  // rotate each workgroup's t-walk (0 = natural order)
 };
 int k5_grid(const Geom& g);
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st);
 // O_k = (D + invL_next*Y_L) - T_{k+1} (O is not stored by K5)
+void launch_pool_probe(const Geom& g, double* D, double* E, double* YL, double* YO, double* T,
+                       hipStream_t st);
 void launch_o_fixup(const Geom& g, const double* D, const double* YL, const double* T,
                     double invL_next, double* O, hipStream_t st);
 // partial sums -> out[0..1] (fixed-order tree)
 void launch_reduce_pairs(const double* partial, int n, double* out, const int* stop, hipStream_t st);
+// both in one launch (single GPU: nothing to all-reduce in between)
+void launch_reduce_finish(const double* partial, int n, double normD, int k, double tol,
+                          double* errHist, double* errL, double* errO, int* ctrl, hipStream_t st);
 // errHist bookkeeping + stop test (triple_decomp_ADMM.m:59,63)
 void launch_finish(const double* ss, double normD, int k, double tol, double* errHist, double* errL,
                    double* errO, int* ctrl, hipStream_t st);

@@ -87,6 +87,8 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     {
         const char* ov = std::getenv("TRITD_OVERLAP");
         ovmode_ = ov ? std::atoi(ov) : 2;
+        const char* rt = std::getenv("TRITD_ROT");
+        rot_ = rt ? std::atoi(rt) : 0;
         if (ovmode_ == 0) overlap_ = false;
     }
     if (overlap_) {
@@ -107,7 +109,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         }
     }
 
-    const size_t Np = (size_t)g_.Np;
+    const size_t Np = (size_t)g_.Ntm;  // tile-major tensors (incl. group padding)
     {
         // the six streamed tensors live in one pool; each base is staggered so
         // that equal offsets of concurrently streamed tensors do not map to
@@ -115,7 +117,9 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         const char* sg = std::getenv("TRITD_STAGGER");
         const size_t stagger = sg ? (size_t)std::atoll(sg) : 256;  // measured: tools/stagger_sweep.py
         const size_t slot = round_up((int64_t)(Np * sizeof(double) + 5 * stagger), 4096);
-        pool_.alloc(6 * slot / sizeof(double));
+        const size_t pool_bytes = 6 * slot;
+        pool_.p = probe_pool(pool_bytes, slot, stagger);
+        pool_.n = pool_bytes / sizeof(double);
         int q = 0;
         for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
             b->p = pool_.p + (q * slot + q * stagger) / sizeof(double);
@@ -193,6 +197,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     a.ntt = g_.ntt;
     a.s = scalars(1);
     a.stop = ctrl_;
+    a.rot = rot_;
     if (o_.maxIter > 0) launch_k5(g_, a, /*prologue=*/true, st_);
     if (overlap_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
         TRITD_HIP(hipEventRecord(evCtC_, st_));
@@ -292,10 +297,70 @@ void Session::phaseC(int k) {
     launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :93 ridge
     launch_apply(RP, red2_.p, g_.n3p, Ginv_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
-    launch_k5_full(k);
+    launch_k5_full(k, /*fused_finish=*/false);
 }
 
-void Session::launch_k5_full(int k) {
+// Placement probing.  K5 is HBM-bound and its bandwidth depends on where the
+// pool lands physically: per allocation it is stable, across allocations it
+// is not (measured 5.1-5.2 vs 5.7-6.05 TB/s for the same pattern, about one
+// allocation in three fast; tools/aos_pattern.hip).  With room to spare,
+// allocate up to TRITD_PROBE (default 8) candidate pools at once, time K5's
+// access pattern on each and keep the fastest.  Results do not depend on the choice (addresses never enter the
+// arithmetic).  Small problems skip it.
+double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
+    const char* pe = std::getenv("TRITD_PROBE");
+    int want = pe ? std::atoi(pe) : 8;
+    if (pool_bytes < ((size_t)1 << 30)) want = 1;
+    size_t fr = 0, tot = 0;
+    TRITD_HIP(hipMemGetInfo(&fr, &tot));
+    // keep room for the chosen pool, the other session buffers and 4 GiB
+    const size_t reserve = pool_bytes / 2 + ((size_t)4 << 30);
+    const size_t room = fr > reserve ? (fr - reserve) / pool_bytes : 0;
+    if ((size_t)want > room) want = room > 1 ? (int)room : 1;
+    std::vector<double*> cand;
+    for (int c = 0; c < want; ++c) {
+        void* p = nullptr;
+        if (hipMalloc(&p, pool_bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        cand.push_back(static_cast<double*>(p));
+    }
+    if (cand.empty()) throw Error(TRITD_ERR_NOMEM, "hipMalloc of the tensor pool failed");
+    probe_ms_.assign(cand.size(), 0.0);
+    size_t best = 0;
+    if (cand.size() > 1) {
+        hipEvent_t e0, e1;
+        TRITD_HIP(hipEventCreate(&e0));
+        TRITD_HIP(hipEventCreate(&e1));
+        for (size_t c = 0; c < cand.size(); ++c) {
+            double* f[6];
+            for (int q = 0; q < 6; ++q) f[q] = cand[c] + (q * slot + q * stagger) / sizeof(double);
+            // pool order: D, O, E, YL, YO, T
+            launch_pool_probe(g_, f[0], f[2], f[3], f[4], f[5], st_);  // warm
+            float ms = 1e30f;
+            for (int r = 0; r < 2; ++r) {
+                TRITD_HIP(hipEventRecord(e0, st_));
+                launch_pool_probe(g_, f[0], f[2], f[3], f[4], f[5], st_);
+                TRITD_HIP(hipEventRecord(e1, st_));
+                TRITD_HIP(hipEventSynchronize(e1));
+                float x = 0.f;
+                TRITD_HIP(hipEventElapsedTime(&x, e0, e1));
+                ms = std::fmin(ms, x);
+            }
+            probe_ms_[c] = ms;
+            if (ms < probe_ms_[best]) best = c;
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    for (size_t c = 0; c < cand.size(); ++c)
+        if (c != best) (void)hipFree(cand[c]);
+    probe_pick_ = (int)best;
+    return cand[best];
+}
+
+void Session::launch_k5_full(int k, bool fused_finish) {
     K5Args a{};
     a.D = D_.p; a.O = O_.p; a.E = E_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
@@ -303,10 +368,15 @@ void Session::launch_k5_full(int k) {
     a.ntt = g_.ntt;
     a.s = scalars(k);
     a.stop = ctrl_;
+    a.rot = rot_;
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
     launch_k5(g_, a, /*prologue=*/false, st_);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 2], st_));
-    launch_reduce_pairs(k5part_.p, k5_grid(g_), red3_.p, ctrl_, st_);
+    if (fused_finish)  // single GPU: no all-reduce between the norm sums and the stop test
+        launch_reduce_finish(k5part_.p, k5_grid(g_), normD_, k, o_.tol, errHist_.p, errL_.p,
+                             errO_.p, ctrl_, st_);
+    else
+        launch_reduce_pairs(k5part_.p, k5_grid(g_), red3_.p, ctrl_, st_);
 }
 
 // Single-GPU iteration.  Same kernels and data flow as phases A-D, but each
@@ -319,21 +389,25 @@ void Session::iterate_overlapped(int k) {
     const int RP = g_.RP;
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
+    // main: M1 -> apply A -> M2 -> apply B -> K2 -> apply C -> K5 -> norms/finish
+    // side: Gram A -> solve B | Gram B -> solve C | Gram C -> solve A(k+1)
+    hipStream_t gs = (ovmode_ >= 3) ? side_ : st_;
     launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
-    if (ovmode_ == 1) launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, st_);
     TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
     launch_apply(RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
-    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    if (gs == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evAtA_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
+    if (gs == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
     launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, GinvB_.p, ctrl_ + 2, ctrl_, side_);
     TRITD_HIP(hipEventRecord(evSB_, side_));
     launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
     TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
     launch_apply(RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, ctrl_, st_);
-    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    if (gs == st_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
+    if (gs == side_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
@@ -341,15 +415,13 @@ void Session::iterate_overlapped(int k) {
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     launch_apply(RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
-    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
-    if (ovmode_ != 1) {
-        TRITD_HIP(hipEventRecord(evCtC_, st_));
-        TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-        launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
-        TRITD_HIP(hipEventRecord(evSA_, side_));
-    }
-    launch_k5_full(k);
-    phaseD(k);
+    if (gs == st_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    TRITD_HIP(hipEventRecord(evCtC_, st_));
+    TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
+    if (gs == side_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+    TRITD_HIP(hipEventRecord(evSA_, side_));
+    launch_k5_full(k, /*fused_finish=*/true);
 }
 
 void Session::phaseD(int k) {

@@ -56,6 +56,8 @@ class Session {
     void rre_parts(const double* dX, int64_t ldX, double* num, double* den);
     void set_timing(bool on);
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
+    const std::vector<double>& probe_ms() const { return probe_ms_; }
+    int probe_pick() const { return probe_pick_; }
 
     // --- phase interface (virtual shard groups drive these directly) ------
     // Returns false when iteration k is beyond maxIter (nothing enqueued).
@@ -81,13 +83,17 @@ class Session {
     // single-GPU schedule: the three R x R solves run on a side stream, each
     // overlapped with the big kernel that precedes its consumer
     void iterate_overlapped(int k);
-    void launch_k5_full(int k);
+    void launch_k5_full(int k, bool fused_finish);
     bool overlap_ = false;
     int ovmode_ = 2;
+    int rot_ = 1;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
     hipEvent_t evSA_ = nullptr, evSB_ = nullptr, evSC_ = nullptr;
     DBuf GinvA_, GinvB_, GinvC_;
+    double* probe_pool(size_t pool_bytes, size_t slot, size_t stagger);
+    std::vector<double> probe_ms_;  // probe time of each candidate pool (ms)
+    int probe_pick_ = 0;
     void upload_factors(const double* A0, const double* B0, const double* C0);
     IterScalars scalars(int k) const;
 

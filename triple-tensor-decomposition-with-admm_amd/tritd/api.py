@@ -259,6 +259,13 @@ class Session:
                                           C.byref(num), C.byref(den)))
         return num.value, den.value
 
+    def probe(self):
+        """(probe ms of each candidate tensor pool, index kept)"""
+        ms = (C.c_double * 16)()
+        n, k = _lib.i32(0), _lib.i32(0)
+        check(lib.tritd_session_probe(self._s, ms, 16, C.byref(n), C.byref(k)))
+        return [ms[i] for i in range(min(n.value, 16))], k.value
+
     def set_timing(self, on=True):
         check(lib.tritd_session_set_timing(self._s, int(bool(on))))
 
