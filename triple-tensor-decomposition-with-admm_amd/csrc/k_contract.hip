@@ -9,6 +9,8 @@
 //            M3(t,k) = sum_ij T(ij,t) A^(i,k) B^(j,k)   MFMA, this file's K2
 // F*F.' = (B^TB) o (C^TC) is the Hadamard identity of the Khatri-Rao design
 // matrices built by buildF/G/H (buildF.m:17-21): F, G, H are never formed.
+#include <utility>
+
 #include "kernels.h"
 
 namespace tritd {
@@ -301,81 +303,117 @@ void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* st
 }
 
 // ---------------------------------------------------------------------------
-// Ginv = inv(P o Q + alpha I): in-place Gauss-Jordan in LDS, one block.
-// The R x R Gram is embedded in an RP x RP matrix with an identity pad, so
-// every thread runs the same branch-free code: thread (column c = th % RP,
-// rows h + G*m).  Two LDS copies ping-pong between pivots, so one barrier
-// per pivot suffices.  The Gram is SPD (ridge alpha > 0): no pivoting.  The
-// smallest Gauss-Jordan pivot (= smallest LDL^T pivot) is compared with
-// MATLAB's pinv tolerance max(size)*eps(max sigma); flags[0] is raised when
-// pinv could truncate (triple_decomp_ADMM.m:78,86,93 use pinv).
+// Ginv = inv(P o Q + alpha I), RP/8 wavefronts, matrix in registers.
+// The R x R matrix is embedded in RP x RP with an identity pad.  It is SPD
+// (ridge alpha > 0), so Gauss-Jordan needs no pivoting, and its symmetric
+// form (the sweep operator) keeps the matrix symmetric at every step, so
+// column P == row P.  Wave w holds rows 8w..8w+7, lane c column c.
+// Sweep on P, D = a_PP:
+//   a_PP <- -1/D,  a_iP <- a_iP/D,  a_Pc <- a_Pc/D,  a_ic <- a_ic - a_iP*(a_Pc/D)
+// after all pivots the matrix is -inv(.).  The off-pivot update is the
+// Gauss-Jordan update term for term; written m*a - f*t with (m, t) = (1, s)
+// or (0, -1/D) it needs no selects and rounds identically.  Per step, every
+// wave publishes its candidate of row P (only the owner's is read), one
+// barrier, double-buffered by step parity (8 rows per lane, RP/8 waves).  The smallest pivot (= smallest
+// LDL^T pivot) is compared with MATLAB's pinv tolerance max(size)*eps(max
+// sigma); flags[0] is raised when pinv could truncate
+// (triple_decomp_ADMM.m:78,86,93 use pinv).
+// Register-pressure notes (each measured): the pivot loop is unrolled via an
+// index sequence (a runtime pivot would index the register array); there is
+// no divergent branch and no per-element runtime mask inside or after the
+// sweep (either made the compiler keep every step's values and spill).
 // ---------------------------------------------------------------------------
-template <int RP>
-struct SolveCfg {
-    static constexpr int NT = (RP == 48) ? 192 : 256;  // threads
-    static constexpr int G = NT / RP;                  // row groups
-    static constexpr int RPT = RP / G;                 // rows per thread
-    static constexpr int LD = RP + 1;
-};
+#ifndef SOLVE_ROWS_OVERRIDE
+constexpr int SOLVE_ROWS = 8;  // matrix rows per lane; RP/8 waves
+#else
+constexpr int SOLVE_ROWS = SOLVE_ROWS_OVERRIDE;  // tools/solve_bench.hip
+#endif
+
+// Sweep step P.  Row P was published (by every wave: its candidate of that
+// local row) into buffer P&1 by the previous step.  All reads are issued
+// first; the row of pivot P+1 is updated before the others and published
+// into the other buffer at once, so the barrier only waits on that.
+template <int RP, int P>
+__device__ __forceinline__ void sweep_step(double (&a)[SOLVE_ROWS], double* rowbuf, double* pivs,
+                                           int c, int w) {
+    constexpr int RW = SOLVE_ROWS, NW = RP / RW, W = P / RW, L = P % RW;
+    const double* row = rowbuf + (P & 1) * NW * 64 + W * 64;  // a_Pc == a_cP
+    const double piv = row[P];
+    const double rc = row[c];
+    double f[RW];  // a_iP for this wave's rows
+#pragma unroll
+    for (int q = 0; q < RW; ++q) f[q] = row[RW * w + q];
+    pivs[P] = piv;  // every thread, same value
+    const double d = 1.0 / piv;
+    const bool pc = (c == P);
+    const double s = rc * d;  // a_Pc / D
+    const double m = pc ? 0.0 : 1.0;
+    const double t = pc ? -d : s;
+    if constexpr (P + 1 < RP) {
+        constexpr int L2 = (P + 1) % RW;
+        a[L2] = m * a[L2] - f[L2] * t;
+        if (L2 == L && w == W) a[L] = t;  // (RW == 1 only)
+        rowbuf[((P + 1) & 1) * NW * 64 + w * 64 + c] = a[L2];
+#pragma unroll
+        for (int q = 0; q < RW; ++q)
+            if (q != L2) a[q] = m * a[q] - f[q] * t;
+    } else {
+#pragma unroll
+        for (int q = 0; q < RW; ++q) a[q] = m * a[q] - f[q] * t;
+    }
+    // row P itself: a_Pc <- a_Pc/D, a_PP <- -1/D
+    if (w == W) a[L] = t;
+    __syncthreads();
+}
+
+template <int RP, int... Ps>
+__device__ __forceinline__ void sweep_all(double (&a)[SOLVE_ROWS], double* rowbuf, double* pivs,
+                                          int c, int w, std::integer_sequence<int, Ps...>) {
+    (sweep_step<RP, Ps>(a, rowbuf, pivs, c, w), ...);
+}
 
 template <int RP>
-__global__ __launch_bounds__(256) void k_solve(const double* __restrict__ P,
-                                               const double* __restrict__ Q, int R, double alpha,
-                                               double* Ginv, int* flags, const int* stop) {
+__global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __restrict__ P,
+                                                               const double* __restrict__ Q,
+                                                               int R, double alpha, double* Ginv,
+                                                               int* flags, const int* stop) {
     if (*stop) return;
-    using S = SolveCfg<RP>;
-    constexpr int G = S::G, RPT = S::RPT, LD = S::LD;
-    __shared__ double M[2][RP * LD];
-    const int th = threadIdx.x;
-    const int c = th % RP, h = th / RP;
+    // runs beside the big kernels (side stream): win instruction issue on
+    // the shared SIMDs, it is on the critical path of the next apply
+    __builtin_amdgcn_s_setprio(3);
+    constexpr int RW = SOLVE_ROWS, NW = RP / RW, NT = NW * 64;
+    __shared__ double rowbuf[2 * NW * 64];
+    __shared__ double pivs[RP];
+    __shared__ double outb[RP * 64];
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cc = c < RP ? c : 0;  // lanes >= RP read a valid column, never written back
+    double a[RW];
 #pragma unroll
-    for (int m = 0; m < RPT; ++m) {
-        const int i = h + G * m;
-        double v;
-        if (i < R && c < R) {
-            v = P[i * RP + c] * Q[i * RP + c];
-            if (i == c) v = v + alpha;
-        } else {
-            v = (i == c) ? 1.0 : 0.0;
-        }
-        M[0][i * LD + c] = v;
+    for (int q = 0; q < RW; ++q) {
+        const int i = RW * w + q;
+        const bool in = (i < R) && (c < R);
+        const double pq = P[i * RP + cc] * Q[i * RP + cc];
+        const double g = (i == c) ? pq + alpha : pq;
+        a[q] = in ? g : ((i == c) ? 1.0 : 0.0);
     }
+    rowbuf[w * 64 + c] = a[0];  // row 0 (wave 0's)
     __syncthreads();
-    double minpiv = 1e308, maxpiv = 0.0;
-    for (int p = 0; p < RP; ++p) {
-        const double* src = M[p & 1];
-        double* dst = M[(p + 1) & 1];
-        const double piv = src[p * LD + p];
-        const double mpc = src[p * LD + c];
-        double mv[RPT], f[RPT];
+    sweep_all<RP>(a, rowbuf, pivs, c, w, std::make_integer_sequence<int, RP>{});
+    // out through LDS, then a linear copy that zeroes the pad (the sweep
+    // leaves the identity-pad block and the zero blocks beside it untouched)
 #pragma unroll
-        for (int m = 0; m < RPT; ++m) {
-            const int i = h + G * m;
-            mv[m] = src[i * LD + c];
-            f[m] = src[i * LD + p];
-        }
-        if (p < R) {
-            minpiv = fmin(minpiv, piv);
-            maxpiv = fmax(maxpiv, piv);
-        }
-        const double d = 1.0 / piv;
-        const double prv = (c == p) ? d : mpc * d;  // new pivot row
-#pragma unroll
-        for (int m = 0; m < RPT; ++m) {
-            const int i = h + G * m;
-            const double base = (c == p) ? 0.0 : mv[m];
-            const double upd = base - f[m] * prv;
-            dst[i * LD + c] = (i == p) ? prv : upd;
-        }
-        __syncthreads();
+    for (int q = 0; q < RW; ++q) outb[(RW * w + q) * 64 + c] = -a[q];
+    __syncthreads();
+    for (int e = threadIdx.x; e < RP * RP; e += NT) {
+        const int i = e / RP, j = e - (e / RP) * RP;
+        Ginv[e] = (i < R && j < R) ? outb[i * 64 + j] : 0.0;
     }
-    const double* fin = M[RP & 1];
-#pragma unroll
-    for (int m = 0; m < RPT; ++m) {
-        const int i = h + G * m;
-        Ginv[i * RP + c] = (i < R && c < R) ? fin[i * LD + c] : 0.0;
-    }
-    if (th == 0) {
+    if (threadIdx.x == 0) {
+        double minpiv = 1e308, maxpiv = 0.0;
+        for (int p = 0; p < R; ++p) {
+            minpiv = fmin(minpiv, pivs[p]);
+            maxpiv = fmax(maxpiv, pivs[p]);
+        }
         // eps(x) = 2^(floor(log2 x) - 52)
         const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);
         if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
@@ -386,7 +424,7 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
                   int* flags, const int* stop, hipStream_t st) {
 #define SOLVE_CASE(RPV)                                                                      \
     case RPV:                                                                                \
-        hipLaunchKernelGGL(k_solve<RPV>, dim3(1), dim3(SolveCfg<RPV>::NT), 0, st, P, Q, R, alpha, \
+        hipLaunchKernelGGL(k_solve<RPV>, dim3(1), dim3(RPV * 64 / SOLVE_ROWS), 0, st, P, Q, R, alpha, \
                            Ginv, flags, stop);                                               \
         break;
     switch (RP) {

@@ -86,7 +86,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     overlap_ = (comm == nullptr) && (shared_stream == nullptr);
     {
         const char* ov = std::getenv("TRITD_OVERLAP");
-        ovmode_ = ov ? std::atoi(ov) : 2;
+        ovmode_ = ov ? std::atoi(ov) : 3;
         const char* rt = std::getenv("TRITD_ROT");
         rot_ = rt ? std::atoi(rt) : 0;
         if (ovmode_ == 0) overlap_ = false;
