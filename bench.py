@@ -79,7 +79,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=N_DEFAULT)
     ap.add_argument("--r", type=int, default=R_DEFAULT)
-    ap.add_argument("--cpu-iters", type=int, default=12)
+    ap.add_argument("--cpu-iters", type=int, default=40)  # ~20 s of host work
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 

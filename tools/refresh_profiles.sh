@@ -1,0 +1,22 @@
+#!/bin/bash
+# Refresh the committed evidence under profiles/ (run through gpurun on one
+# MI355X; outputs land in gpurun_out/ and are copied into profiles/ locally):
+#   two separate PMC passes (FETCH_SIZE, WRITE_SIZE) -> K5 HBM bytes per launch
+#   rocprofv3 --kernel-trace --stats of the default bench
+#   the default bench line (with cpu_baseline), reading the fresh traffic file
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=${1:-r01}
+ALG=${2:-8724152320}   # K5 algorithmic bytes per launch
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- \
+    python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- \
+    python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/pmc_write.log 2>&1
+python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/${TAG}_k5_traffic.json $ALG
+cp $O/${TAG}_k5_traffic.json profiles/${TAG}_k5_traffic.json   # read by bench.py below
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
+    python3 bench.py --no-cpu > $O/stats.log 2>&1
+timeout -k 10 400 python3 bench.py > $O/${TAG}_bench_line.json 2> $O/bench.err
+cat $O/${TAG}_bench_line.json
