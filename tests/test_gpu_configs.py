@@ -161,3 +161,31 @@ def test_config4_pool_probe_does_not_change_results(tritd, big, monkeypatch):
         s.close()
     for key in ("A", "B", "C", "O", "E", "errHist"):
         np.testing.assert_array_equal(out[0][key], out[1][key])
+
+
+@pytest.mark.parametrize("case", ["mixed_tiles", "all_dense"])
+def test_compact_e_overflow_tiles_vs_c_oracle(tritd, cref, case):
+    """E lives in a compact per-tile form with a dense fallback for tiles with
+    more than 28 nonzeros (common.h: CE).  mixed_tiles: a block of dense
+    outliers makes some tiles overflow while the rest stay compact, and tiles
+    switch form across iterations; all_dense: a tiny lambda makes E dense
+    everywhere.  Both against the C restatement."""
+    from tritd import synth
+    mod, lib = cref
+    n1, n2, n3, r = 48, 20, 64, 3
+    d = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=11, init_seed=5)
+    D = d["D"].copy(order="F")
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=30)
+    if case == "mixed_tiles":
+        rng = np.random.default_rng(3)
+        D[:16, :7, :40] += 8.0 * rng.standard_normal((16, 7, 40))
+    else:
+        opts["lambda"] = 1e-6
+    ref = mod.admm(lib, D, r, opts, d["A0"], d["B0"], d["C0"])
+    A, B, C, O, eh, E, k = tritd.triple_decomp_ADMM(D, r, opts, d["A0"], d["B0"], d["C0"],
+                                                    return_E=True, return_iters=True)
+    assert k == ref[6]
+    nnz = np.count_nonzero(E) / E.size
+    assert (nnz > 0.5) if case == "all_dense" else (0.02 < nnz < 0.5)
+    assert rel(O, ref[3]) <= 1e-9 and rel(E, ref[5]) <= 1e-9
+    np.testing.assert_allclose(eh, ref[4], rtol=1e-8, atol=ATOL_ERR)

@@ -18,16 +18,21 @@ for p in paths:
         fn = getattr(l, name); fn.restype = res; fn.argtypes = args
     libs[p] = l
 n, r = 512, 8
-rng = np.random.default_rng(0)
-D = np.asfortranarray(rng.standard_normal((n, n, n)))
-A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
+if os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere (worst case for CE)
+    rng = np.random.default_rng(0)
+    D = np.asfortranarray(rng.standard_normal((n, n, n)))
+    A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
+else:  # the bench workload (low rank + 5 % outliers)
+    dd = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
+    D, A0, B0, C0 = dd["D"], dd["A0"], dd["B0"], dd["C0"]
+warm = int(os.environ.get("AB_WARM", "15"))
 opts = dict(synth.TRAFFIC_OPTS, maxIter=100, tol=float(os.environ.get("AB_TOL", "1e-5")))
 res = {p: [] for p in paths}
 for rep in range(reps):
     for p in paths:
         api.lib = _lib.lib = libs[p]
         s = tritd.Session(r, opts, A0, B0, C0, n1=n, n2=n, n3=n, D=D, device=0)
-        s.run(2); s.sync(); s.set_timing(True); s.run(iters); s.sync()
+        s.run(warm); s.sync(); s.set_timing(True); s.run(iters); s.sync()
         km = s.kernel_ms()
         pr = s.probe() if hasattr(libs[p], "tritd_session_probe") else None
         res[p].append((km["iteration"], km["fused_update"], km["mode3"]))

@@ -48,6 +48,40 @@ __global__ __launch_bounds__(256) void k_pat(double* base, long fstride, long ti
     else body(tt, xa, xb, false);
 }
 
+// compact-E variant: reads D, YL, YO + the tile's 256 B slot (8 B per lane,
+// lanes 32..63 duplicate), writes YL, YO, T + the slot (lanes 0..31)
+__global__ __launch_bounds__(256) void k_ce(double* base, long fstride, long tiles, long ntt) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const long tile = (long)blockIdx.x * 4 + wid;
+    d2v* F[5];
+    for (int f = 0; f < 5; ++f) F[f] = reinterpret_cast<d2v*>(base + f * fstride);
+    double* CE = base + 5 * fstride;  // slots: 32 doubles per tile
+    auto off = [&](long tt) { return (tbase<0>(tile, tt, ntt, tiles / 4) >> 1) + lane; };
+    auto so = [&](long tt) { return (tbase<0>(tile, tt, ntt, tiles / 4) >> 8) * 32 + (lane & 31); };
+    struct R { d2v x[3][2]; double c; };
+    R xa, xb;
+    auto ld = [&](long tt, R& n) {
+        const long o = off(tt);
+        for (int p = 0; p < 2; ++p) { n.x[0][p] = F[0][o + 64 * p]; n.x[1][p] = F[1][o + 64 * p]; n.x[2][p] = F[3][o + 64 * p]; }
+        n.c = CE[so(tt)];
+    };
+    auto body = [&](long tt, R& c, R& n, bool pf) {
+        if (pf) { ld(tt + 1, n); __builtin_amdgcn_sched_barrier(0); }
+        const long o = off(tt);
+        for (int p = 0; p < 2; ++p) {
+            F[1][o + 64 * p] = c.x[0][p] + c.x[1][p];
+            F[3][o + 64 * p] = c.x[2][p] - c.x[1][p];
+            F[4][o + 64 * p] = c.x[0][p] * c.x[2][p];
+        }
+        if (lane < 32) CE[so(tt)] = c.c + 1.0;
+    };
+    ld(0, xa);
+    long tt = 0;
+    for (; tt + 2 < ntt; tt += 2) { body(tt, xa, xb, true); body(tt + 1, xb, xa, true); }
+    if (tt + 1 < ntt) { body(tt, xa, xb, true); body(tt + 1, xb, xa, false); }
+    else body(tt, xa, xb, false);
+}
+
 __global__ __launch_bounds__(256) void k_lin(double* base, long fstride, long tiles, long ntt) {
     d2v* F[5];
     for (int f = 0; f < 5; ++f) F[f] = reinterpret_cast<d2v*>(base + f * fstride);
@@ -62,8 +96,7 @@ int main() {
     const long ntt = 32, tiles = 16384;  // 512^3 doubles
     const long N = tiles * ntt * 256;    // doubles per field
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    const double bytes = 8.0 * N * 8;
-    auto time = [&](auto kern, int grid, double* base, long fstride, const char* name, int rep) {
+    auto time = [&](auto kern, int grid, double* base, long fstride, const char* name, int rep, double bytes = 8.0 * N * 8) {
         float ms = 0, best = 1e9;
         for (int r = 0; r < 4; ++r) {
             hipEventRecord(e0);
@@ -79,8 +112,7 @@ int main() {
     for (auto& p : pools) { CK(hipMalloc(&p, 6 * fstride * 8)); CK(hipMemset(p, 0, 6 * fstride * 8)); }
     for (int k = 0; k < K; ++k) {
         time(k_pat<0>, tiles / 4, pools[k], fstride, "GM", k);
-        time(k_pat<1>, tiles / 4, pools[k], fstride, "TM", k);
-        time(k_lin, 8192, pools[k], fstride, "LIN", k);
+        time(k_ce, tiles / 4, pools[k], fstride, "CE", k, 6.0 * N * 8 + 2.0 * N);
     }
     for (auto p : pools) hipFree(p);
     return 0;

@@ -96,6 +96,20 @@ struct IterScalars {
 };
 
 // first double of tile (g, tt) in the tile-major layout
+// Compact E (CE).  E is the soft-thresholded outlier tensor, mostly zeros
+// (<= 5 % nonzero and <= 33 per 256-element tile on the bench workload), so
+// it is kept as one 32-double slot per tile (slot of tile ordinal b =
+// tm_tile_base(g, tt)/256 at CE + 32 b):
+//   words 0..3: bit masks; bit l of word w <=> the element lane l holds as
+//               MFMA C/D register element (p, q) = (w >> 1, w & 1), i.e. the
+//               TM in-tile position 128 p + 2 l + q, is nonzero
+//   words 4..31: the nonzero values, ordered by (w, l)
+// A tile with more than CE_CAP nonzeros is stored densely in E (TM) and its
+// slot masks are all ones.  Zeros are stored as +0 (MATLAB's E may hold -0,
+// which is numerically identical in every later use).
+constexpr int CE_SLOT = 32;
+constexpr int CE_CAP = CE_SLOT - 4;
+
 __host__ __device__ inline int64_t tm_tile_base(int64_t g, int64_t tt, int64_t ntt) {
     return ((((g >> 2) * ntt + tt) << 2) + (g & 3)) << 8;
 }

@@ -8,8 +8,9 @@
 //   ||resL||^2, ||resO||^2                       :59
 //   T_next = D - O + (1/muL_next)*Y_L            :33 of the NEXT iteration
 //   W(ij,k) = sum_t T_next(ij,t) C^(t,k)         mode-1/2 half of update_A/update_B (:78,:86)
-// in one pass: reads D, Y_L, E, Y_O and writes E, Y_L, Y_O, T (8 N-streams)
-// plus W (N*R/n3 elements).  O is never read inside the loop (E, not O, feeds
+// in one pass: reads D, Y_L, Y_O and writes Y_L, Y_O, T (6 N-streams), reads
+// and writes E in its compact form (one 256 B slot per 2 KB tile, common.h;
+// dense only for overflowed tiles), plus W (N*R/n3 elements).  O is never read inside the loop (E, not O, feeds
 // :42), so it is not stored: T_{k+1} = (D - O_k) + Y_L/muL_{k+1} determines it
 // and k_o_fixup rebuilds O_k = (D + Y_L/muL_{k+1}) - T_{k+1} when the caller
 // asks for it (relative error ~1e-16).
@@ -66,8 +67,107 @@ __device__ __forceinline__ void st2(d2v v, d2v* p) {
         *p = v;
 }
 
+// --- compact E (common.h: CE) -------------------------------------------
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+constexpr int OOB = 0x40000000;  // buffer offset past any range: the access is dropped (loads give 0)
+
+// buffer descriptor of `bytes` bytes at p (p made wave-uniform explicitly, so
+// the descriptor lives in SGPRs without a waterfall loop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, int bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ uint64_t ce_word(double sv, int w) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(__double2loint(sv), w);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(__double2hiint(sv), w);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ bool ce_is_dense(double sv) {
+    return (ce_word(sv, 0) & ce_word(sv, 1) & ce_word(sv, 2) & ce_word(sv, 3)) == ~0ull;
+}
+// This lane's 4 elements (register order r = 2p+q) from its slot double sv
+// (lane l holds slot word l & 31).  Returns true for a dense (overflowed)
+// tile, whose values are in E instead.
+__device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
+    uint64_t m[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) m[w] = ce_word(sv, w);
+    const int svlo = __double2loint(sv), svhi = __double2hiint(sv);
+    int pre = 4;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int src = (pre + lanes_below(m[w])) & 63;
+        const int vlo = __builtin_amdgcn_ds_bpermute(src << 2, svlo);
+        const int vhi = __builtin_amdgcn_ds_bpermute(src << 2, svhi);
+        e[w] = ((m[w] >> lane) & 1) ? __hiloint2double(vhi, vlo) : 0.0;
+        pre += __builtin_popcountll(m[w]);
+    }
+    return (m[0] & m[1] & m[2] & m[3]) == ~0ull;
+}
+// Store this lane's 4 elements of E (register order) as the tile's slot at
+// CE + sb, or densely into E2 at d2v offset o when they do not fit.  cs: the
+// wave's 96-double LDS scratch (slot image + a junk area for the zeros).
+// Branch-free: a branch here makes the compiler's vmcnt waits drain the
+// prefetch.
+__device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, double* cs, double* CE,
+                                          int64_t sb, d2v* E2, int64_t o) {
+    uint64_t nz[4];
+    int cnt = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        nz[w] = __ballot(En[w] != 0.0);
+        cnt += __builtin_popcountll(nz[w]);
+    }
+    const int l = lane & 31;
+    const bool dense = cnt > CE_CAP;
+    // slot image: zeros, then the packed values, then the masks (all lanes
+    // write the same mask words: no lane test)
+    cs[l < 4 ? 32 + lane : l] = 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    int pre = 4;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        // (a dense tile's image is not used: its values go to the junk area,
+        // they would index past the scratch)
+        const int bit = dense ? 0 : (int)((nz[w] >> lane) & 1);
+        const int at = pre + lanes_below(nz[w]), away = 32 + lane;
+        cs[away + ((at - away) & -bit)] = En[w];
+        pre += __builtin_popcountll(nz[w]);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) cs[w] = __longlong_as_double(dense ? -1ll : (long long)nz[w]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const double v = cs[l];
+    // the dense tile (only when it does not fit) and the slot (lanes 0..31):
+    // out-of-range buffer offsets drop the other stores, no branch
+    if (!(K5_EXP & 16)) {  // (timing-only builds drop the dense-E instructions)
+    const __amdgpu_buffer_rsrc_t rt = wave_rsrc(E2 + (o - lane), 2048);
+    const int od = dense ? lane * 16 : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{En[0], En[1]}), rt, od, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{En[2], En[3]}), rt, od + 1024,
+                                           0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(CE + sb, CE_SLOT * 8);
+    const double sv = (dense && l >= 4) ? 0.0 : v;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, sv), rs, lane < 32 ? l * 8 : OOB,
+                                          0, 0);
+}
+
+// Two waves per SIMD (VGPRs + AGPRs <= 256): at one wave per SIMD the
+// streams do not keep enough bytes in flight (measured +6 % K5 time).
 template <int RP, bool PRO>
-__global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
+__global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k5_fused(K5Args a) {
     if (*a.stop) return;
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
@@ -151,38 +251,72 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
     d2v* YO2 = reinterpret_cast<d2v*>(a.YO);
     d2v* T2 = reinterpret_cast<d2v*>(a.T);
 
-    // Two register sets [0] = D, [1] = Y_L, [2] = E (PRO: O), [3] = Y_O.  The
-    // t-walk is unrolled by two so that the sets alternate by name: a copy
-    // cur = next would make the compiler wait for the prefetch at the copy.
-    // Inside the walk nothing depends on `active` (a wave past the last tile
-    // streams the zero-filled group padding, see common.h), so the
-    // steady-state loop has no control-flow joins and the in-order vmcnt
-    // waits stay exact.
-    auto load = [&](int64_t tt, d2v (&nx)[4][2]) {
+    // Two register sets: x[0] = D, x[1] = Y_L, x[2] = Y_O (PRO: O), ed = the
+    // tile's dense E (only meaningful for an overflowed tile) and ce = the
+    // lane's word of a compact-E slot.  The t-walk is unrolled by two so that
+    // the sets alternate by name: a copy cur = next would make the compiler
+    // wait for the prefetch at the copy.  Slots are loaded two tiles ahead,
+    // so when tile tt+1's batch is issued it is already known whether that
+    // tile is dense; its dense E load is issued either way, as a buffer load
+    // whose offset is out of range unless it is (no traffic), so the walk has
+    // no branches at all (a join
+    // makes the compiler's in-order vmcnt waits conservative, i.e. it waits
+    // on the batch it just issued).  Nothing depends on `active` either (a
+    // wave past the last tile streams the zero-filled group padding).
+    struct Regs {
+        d2v x[3][2];
+        d2v ed[2];
+        double ce;
+    };
+    __shared__ double csm[K5_WAVES][96];
+    double* cs = csm[wid];
+    auto load = [&](int64_t tt, Regs& nx) {
         const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            nx[0][p] = ld2(D2 + o + 64 * p);
-            nx[1][p] = ld2(YL2 + o + 64 * p);
-            if (PRO) {
-                nx[2][p] = ld2(O2 + o + 64 * p);
-            } else {
-                nx[2][p] = ld2(E2 + o + 64 * p);
-                nx[3][p] = ld2(YO2 + o + 64 * p);
-            }
+            nx.x[0][p] = ld2(D2 + o + 64 * p);
+            nx.x[1][p] = ld2(YL2 + o + 64 * p);
+            nx.x[2][p] = ld2((PRO ? O2 : YO2) + o + 64 * p);
         }
+    };
+    auto load_dense = [&](int64_t tt, Regs& nx, bool dn) {  // zeros unless dn (no traffic)
+        const __amdgpu_buffer_rsrc_t rt = wave_rsrc(E2 + (tm_tile_base(tile, phys(tt), ntt) >> 1), 2048);
+        const int od = dn ? lane * 16 : OOB;
+        if (!(K5_EXP & 16))
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            nx.ed[p] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rt, od + 1024 * p, 0, 0));
+    };
+    auto load_slot = [&](int64_t tt, double& ce) {
+        const int64_t t2 = tt < ntt ? tt : ntt - 1;  // clamped: no branch
+        ce = a.CE[(tm_tile_base(tile, phys(t2), ntt) >> 8) * CE_SLOT + (lane & 31)];
     };
     // one t-tile: cx holds its data; if `pf`, tile tt+1 is prefetched into nx
     // and its C^ slice staged into buffer buf^1
-    auto body = [&](int64_t tt, int buf, d2v (&cx)[4][2], d2v (&nx)[4][2], bool pf) {
+    auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+        const int64_t tb = tm_tile_base(tile, phys(tt), ntt);
+        const int64_t o = (tb >> 1) + lane;
+        // prefetch first; it only needs tile tt+1's dense flag, whose slot
+        // arrived with the batch of this tile
         if (pf) {
+            const bool dn1 = PRO ? false : ce_is_dense(nx.ce);
             stage_load(tt + 1);
             load(tt + 1, nx);
-            // keep the prefetch at the top: the scheduler otherwise sinks it
-            // next to the stores (less register pressure, no latency hiding)
+            if (!PRO) load_dense(tt + 1, nx, dn1);
+            // keep the prefetch ahead of the compute: the scheduler otherwise
+            // sinks it next to the stores (less register pressure, no latency
+            // hiding)
             __builtin_amdgcn_sched_barrier(0);
         }
-        const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
+        double ev[4];
+        if (!PRO) {
+            const bool dn = ce_decode(cx.ce, lane, ev);
+            ev[0] = dn ? cx.ed[0][0] : ev[0];
+            ev[1] = dn ? cx.ed[0][1] : ev[1];
+            ev[2] = dn ? cx.ed[1][0] : ev[2];
+            ev[3] = dn ? cx.ed[1][1] : ev[3];
+            if (pf) load_slot(tt + 2, cx.ce);  // cx.ce was consumed above
+        }
         const double* cT = sCT[buf];
         const double* cR = sC[buf];
         double tr[4];
@@ -191,7 +325,7 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
             for (int p = 0; p < 2; ++p) {
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    const double d = cx[0][p][q], yl = cx[1][p][q], ov = cx[2][p][q];
+                    const double d = cx.x[0][p][q], yl = cx.x[1][p][q], ov = cx.x[2][p][q];
                     const double tn = (d - ov) + sc.invL * yl;  // :33
                     tr[2 * p + q] = tn;
                 }
@@ -201,36 +335,37 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
             if (!(K5_EXP & 1))
 #pragma unroll
                 for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
+            double En[4];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                d2v En2, YLn2, YOn2;
+                d2v YLn2, YOn2;
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int r = 2 * p + q;
-                    const double d = cx[0][p][q], yl = cx[1][p][q], e = cx[2][p][q],
-                                 yo = cx[3][p][q];
+                    const double d = cx.x[0][p][q], yl = cx.x[1][p][q], e = ev[r],
+                                 yo = cx.x[2][p][q];
                     const double L = lacc[r];
                     const double R1 = (d - L) + sc.invL * yl;               // :41
                     const double R2 = e - sc.invO * yo;                     // :42
                     const double On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
                     const double R3 = On + sc.invO * yo;                    // :46
-                    const double En = matlab_sign(R3) * fmax(fabs(R3) - sc.thr, 0.0);  // :47
+                    const double Ev = matlab_sign(R3) * fmax(fabs(R3) - sc.thr, 0.0);  // :47
                     const double rL = (d - L) - On;                         // :50
-                    const double rO = On - En;                              // :51
+                    const double rO = On - Ev;                              // :51
                     const double YLn = yl + sc.muL * rL;                    // :52
                     const double YOn = yo + sc.muO * rO;                    // :53
                     const double Tn = (d - On) + sc.invL_next * YLn;        // :33 (k+1)
                     ssL += rL * rL;
                     ssO += rO * rO;
-                    En2[q] = En;
+                    En[r] = Ev;
                     YLn2[q] = YLn;
                     YOn2[q] = YOn;
                     tr[r] = Tn;
                 }
-                st2(En2, E2 + o + 64 * p);
                 st2(YLn2, YL2 + o + 64 * p);
                 st2(YOn2, YO2 + o + 64 * p);
             }
+            ce_encode(En, lane, cs, a.CE, (tb >> 8) * CE_SLOT, E2, o);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
         if (K5_EXP & 8) {
@@ -262,12 +397,22 @@ __global__ __launch_bounds__(64 * K5_WAVES) void k5_fused(K5Args a) {
         }
         if (pf) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
         if (!(K5_EXP & 4)) __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
+        // step boundary: the scheduler would otherwise hoist the next step's
+        // dense-slot test (which needs this step's loads) above the barrier
+        __builtin_amdgcn_sched_barrier(0);
     };
 
-    d2v xa[4][2], xb[4][2];
+    Regs xa, xb;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) xa[q][0] = xa[q][1] = xb[q][0] = xb[q][1] = d2v{0.0, 0.0};
+    for (int q = 0; q < 3; ++q) xa.x[q][0] = xa.x[q][1] = xb.x[q][0] = xb.x[q][1] = d2v{0.0, 0.0};
+    xa.ed[0] = xa.ed[1] = xb.ed[0] = xb.ed[1] = d2v{0.0, 0.0};
+    xa.ce = xb.ce = 0.0;
+    if (!PRO) {
+        load_slot(0, xa.ce);
+        load_slot(1, xb.ce);
+    }
     load(0, xa);
+    if (!PRO) load_dense(0, xa, ce_is_dense(xa.ce));
     stage(0, 0);
     __syncthreads();
     int64_t tt = 0;
@@ -457,41 +602,47 @@ void launch_o_fixup(const Geom& g, const double* D, const double* YL, const doub
     TRITD_CHECK_LAUNCH();
 }
 
-// Placement probe: K5's exact HBM pattern (read D, Y_L, E, Y_O; write E, Y_L,
-// Y_O in place and T; one wave per ij-tile walking its t-tiles, prefetched)
-// without the arithmetic.  K5 is HBM-bound (dropping all its compute leaves
-// its time unchanged) and its bandwidth depends on where the pool landed
-// physically; the session times candidate pools with this and keeps the
-// fastest.  Contents are overwritten with garbage.
-__global__ __launch_bounds__(256) void k_pool_probe(double* D, double* E, double* YL, double* YO,
-                                                    double* T, int64_t tiles4, int64_t ntt) {
+// Placement probe: K5's HBM pattern (read D, Y_L, Y_O and the tile's 256 B
+// compact-E slot; write Y_L, Y_O in place, T and the slot; one wave per
+// ij-tile walking its t-tiles, prefetched) without the arithmetic.  K5 is
+// HBM-bound (dropping all its compute leaves its time unchanged) and its
+// bandwidth depends on where the pool landed physically; the session times
+// candidate pools with this and keeps the fastest.  Contents
+// are overwritten with garbage.
+__global__ __launch_bounds__(256) void k_pool_probe(double* D, double* YL, double* YO, double* T,
+                                                    double* CE, int64_t tiles4, int64_t ntt) {
     const int lane = threadIdx.x & 63;
     const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= tiles4) return;
-    d2v* P[5] = {reinterpret_cast<d2v*>(D), reinterpret_cast<d2v*>(YL), reinterpret_cast<d2v*>(E),
-                 reinterpret_cast<d2v*>(YO), reinterpret_cast<d2v*>(T)};
-    auto off = [&](int64_t tt) { return (tm_tile_base(tile, tt, ntt) >> 1) + lane; };
-    d2v xa[4][2], xb[4][2];
-    auto load = [&](int64_t tt, d2v (&nx)[4][2]) {
-        const int64_t o = off(tt);
+    d2v* P[4] = {reinterpret_cast<d2v*>(D), reinterpret_cast<d2v*>(YL), reinterpret_cast<d2v*>(YO),
+                 reinterpret_cast<d2v*>(T)};
+    auto tb = [&](int64_t tt) { return tm_tile_base(tile, tt, ntt); };
+    struct R {
+        d2v x[3][2];
+        double ce;
+    };
+    R xa, xb;
+    auto load = [&](int64_t tt, R& nx) {
+        const int64_t o = (tb(tt) >> 1) + lane;
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int f = 0; f < 4; ++f) nx[f][p] = P[f][o + 64 * p];
+            for (int f = 0; f < 3; ++f) nx.x[f][p] = P[f][o + 64 * p];
+        nx.ce = CE[(tb(tt) >> 8) * CE_SLOT + (lane & 31)];
     };
-    auto body = [&](int64_t tt, d2v (&c)[4][2], d2v (&n)[4][2], bool pf) {
+    auto body = [&](int64_t tt, R& c, R& n, bool pf) {
         if (pf) {
             load(tt + 1, n);
             __builtin_amdgcn_sched_barrier(0);
         }
-        const int64_t o = off(tt);
+        const int64_t o = (tb(tt) >> 1) + lane;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            P[1][o + 64 * p] = c[0][p] + c[1][p];
-            P[2][o + 64 * p] = c[2][p] - c[3][p];
-            P[3][o + 64 * p] = c[1][p] - c[3][p];
-            P[4][o + 64 * p] = c[0][p] - c[2][p];
+            P[1][o + 64 * p] = c.x[0][p] + c.x[1][p];
+            P[2][o + 64 * p] = c.x[2][p] - c.x[1][p];
+            P[3][o + 64 * p] = c.x[0][p] - c.x[2][p];
         }
+        CE[(tb(tt) >> 8) * CE_SLOT + (lane & 31)] = c.ce + 1.0;
     };
     load(0, xa);
     int64_t tt = 0;
@@ -507,10 +658,31 @@ __global__ __launch_bounds__(256) void k_pool_probe(double* D, double* E, double
     }
 }
 
-void launch_pool_probe(const Geom& g, double* D, double* E, double* YL, double* YO, double* T,
+void launch_pool_probe(const Geom& g, double* D, double* YL, double* YO, double* T, double* CE,
                        hipStream_t st) {
-    hipLaunchKernelGGL(k_pool_probe, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D, E, YL, YO,
-                       T, g.tiles4, g.ntt);
+    hipLaunchKernelGGL(k_pool_probe, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D, YL, YO, T,
+                       CE, g.tiles4, g.ntt);
+    TRITD_CHECK_LAUNCH();
+}
+
+// Compact E -> dense E (TM) for every tile that is not already dense: one
+// wave per tile ordinal (common.h: CE).
+__global__ __launch_bounds__(256) void k_ce_expand(const double* __restrict__ CE, double* E,
+                                                   int64_t ntiles) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= ntiles) return;
+    const double sv = CE[b * CE_SLOT + (lane & 31)];
+    double e[4];
+    if (ce_decode(sv, lane, e)) return;  // dense tile: E already holds it
+    d2v* E2 = reinterpret_cast<d2v*>(E) + b * 128 + lane;
+    E2[0] = d2v{e[0], e[1]};
+    E2[64] = d2v{e[2], e[3]};
+}
+
+void launch_ce_expand(const Geom& g, const double* CE, double* E, hipStream_t st) {
+    const int64_t ntiles = g.Ntm / 256;
+    hipLaunchKernelGGL(k_ce_expand, dim3((unsigned)cdiv(ntiles, 4)), dim3(256), 0, st, CE, E, ntiles);
     TRITD_CHECK_LAUNCH();
 }
 

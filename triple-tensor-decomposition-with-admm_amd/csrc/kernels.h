@@ -14,7 +14,8 @@ struct DevState;  // solver.cpp
 struct K5Args {
     const double* D;
     double* O;
-    double* E;
+    double* E;   // dense E: only tiles whose compact slot overflowed (common.h)
+    double* CE;  // compact E: one 32-double slot per tile
     double* YL;
     double* YO;
     double* T;
@@ -32,8 +33,9 @@ struct K5Args {
 int k5_grid(const Geom& g);
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st);
 // O_k = (D + invL_next*Y_L) - T_{k+1} (O is not stored by K5)
-void launch_pool_probe(const Geom& g, double* D, double* E, double* YL, double* YO, double* T,
+void launch_pool_probe(const Geom& g, double* D, double* YL, double* YO, double* T, double* CE,
                        hipStream_t st);
+void launch_ce_expand(const Geom& g, const double* CE, double* E, hipStream_t st);
 void launch_o_fixup(const Geom& g, const double* D, const double* YL, const double* T,
                     double invL_next, double* O, hipStream_t st);
 // partial sums -> out[0..1] (fixed-order tree)

@@ -118,7 +118,9 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         const size_t stagger = sg ? (size_t)std::atoll(sg) : 256;  // measured: tools/stagger_sweep.py
         const size_t slot = round_up((int64_t)(Np * sizeof(double) + 5 * stagger), 4096);
         const size_t pool_bytes = 6 * slot;
+        CE_.alloc((size_t)(g_.Ntm / 256) * CE_SLOT);  // before probing: the probe streams it
         pool_.p = probe_pool(pool_bytes, slot, stagger);
+        TRITD_HIP(hipMemsetAsync(CE_.p, 0, CE_.n * sizeof(double), st_));
         pool_.n = pool_bytes / sizeof(double);
         int q = 0;
         for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
@@ -191,7 +193,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
 
     // T of iteration 1 (:33) and W = T x3 C0 for update_A/update_B
     K5Args a{};
-    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.CE = CE_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
     a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
     a.ntt = g_.ntt;
@@ -337,11 +339,11 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
             double* f[6];
             for (int q = 0; q < 6; ++q) f[q] = cand[c] + (q * slot + q * stagger) / sizeof(double);
             // pool order: D, O, E, YL, YO, T
-            launch_pool_probe(g_, f[0], f[2], f[3], f[4], f[5], st_);  // warm
+            launch_pool_probe(g_, f[0], f[3], f[4], f[5], CE_.p, st_);  // warm
             float ms = 1e30f;
             for (int r = 0; r < 2; ++r) {
                 TRITD_HIP(hipEventRecord(e0, st_));
-                launch_pool_probe(g_, f[0], f[2], f[3], f[4], f[5], st_);
+                launch_pool_probe(g_, f[0], f[3], f[4], f[5], CE_.p, st_);
                 TRITD_HIP(hipEventRecord(e1, st_));
                 TRITD_HIP(hipEventSynchronize(e1));
                 float x = 0.f;
@@ -362,7 +364,7 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
 
 void Session::launch_k5_full(int k, bool fused_finish) {
     K5Args a{};
-    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.CE = CE_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
     a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
     a.ntt = g_.ntt;
@@ -535,6 +537,7 @@ void Session::get(double* A, double* B, double* C, double* O, double* E, int64_t
     }
     if (O && g_.n1l > 0 && done > 0)  // O of iteration `done` from D, Y_L, T (K5 does not store it)
         launch_o_fixup(g_, D_.p, YL_.p, T_.p, 1.0 / mu_[(size_t)done], O_.p, st_);
+    if (E && g_.n1l > 0) launch_ce_expand(g_, CE_.p, E_.p, st_);  // E lives in compact form
     if ((O || E) && g_.n1l > 0) {
         DBuf tmp;
         tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));

@@ -109,6 +109,7 @@ class Session {
 
     DBuf pool_;  // declared first: destroyed after the views into it
     DBuf D_, O_, E_, YL_, YO_, T_, Wk_;
+    DBuf CE_;  // compact E slots (common.h)
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;
