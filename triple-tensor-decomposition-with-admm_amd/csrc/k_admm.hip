@@ -148,14 +148,12 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const double v = cs[l];
-    // the dense tile (only when it does not fit) and the slot (lanes 0..31):
-    // out-of-range buffer offsets drop the other stores, no branch
-    if (!(K5_EXP & 16)) {  // (timing-only builds drop the dense-E instructions)
-    const __amdgpu_buffer_rsrc_t rt = wave_rsrc(E2 + (o - lane), 2048);
-    const int od = dense ? lane * 16 : OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{En[0], En[1]}), rt, od, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{En[2], En[3]}), rt, od + 1024,
-                                           0, 0);
+    // the dense tile only when it does not fit (wave-uniform, rare: a branch
+    // with stores only leaves the common path's waits exact), the slot from
+    // lanes 0..31 (an out-of-range offset drops the rest)
+    if (dense) {
+        E2[o] = d2v{En[0], En[1]};
+        E2[o + 64] = d2v{En[2], En[3]};
     }
     const __amdgpu_buffer_rsrc_t rs = wave_rsrc(CE + sb, CE_SLOT * 8);
     const double sv = (dense && l >= 4) ? 0.0 : v;
@@ -279,13 +277,10 @@ void k5_fused(K5Args a) {
             nx.x[2][p] = ld2((PRO ? O2 : YO2) + o + 64 * p);
         }
     };
-    auto load_dense = [&](int64_t tt, Regs& nx, bool dn) {  // zeros unless dn (no traffic)
-        const __amdgpu_buffer_rsrc_t rt = wave_rsrc(E2 + (tm_tile_base(tile, phys(tt), ntt) >> 1), 2048);
-        const int od = dn ? lane * 16 : OOB;
-        if (!(K5_EXP & 16))
+    auto load_dense = [&](int64_t tt, Regs& nx) {
+        const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-            nx.ed[p] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rt, od + 1024 * p, 0, 0));
+        for (int p = 0; p < 2; ++p) nx.ed[p] = E2[o + 64 * p];
     };
     auto load_slot = [&](int64_t tt, double& ce) {
         const int64_t t2 = tt < ntt ? tt : ntt - 1;  // clamped: no branch
@@ -302,11 +297,14 @@ void k5_fused(K5Args a) {
             const bool dn1 = PRO ? false : ce_is_dense(nx.ce);
             stage_load(tt + 1);
             load(tt + 1, nx);
-            if (!PRO) load_dense(tt + 1, nx, dn1);
             // keep the prefetch ahead of the compute: the scheduler otherwise
             // sinks it next to the stores (less register pressure, no latency
             // hiding)
             __builtin_amdgcn_sched_barrier(0);
+            // rare, wave-uniform: tile tt+1 overflowed last time.  Issued after
+            // the batch and consumed a step later, so the common path's waits
+            // stay exact
+            if (!PRO && dn1) load_dense(tt + 1, nx);
         }
         double ev[4];
         if (!PRO) {
@@ -412,7 +410,7 @@ void k5_fused(K5Args a) {
         load_slot(1, xb.ce);
     }
     load(0, xa);
-    if (!PRO) load_dense(0, xa, ce_is_dense(xa.ce));
+    if (!PRO && ce_is_dense(xa.ce)) load_dense(0, xa);
     stage(0, 0);
     __syncthreads();
     int64_t tt = 0;
