@@ -127,6 +127,7 @@ def main():
     sess.run(W)
     sess.sync()
     sess.set_timing(True)
+    dense0, tiles_per_launch = sess.counters()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -137,6 +138,8 @@ def main():
     dt = time.perf_counter() - t0
     km = sess.kernel_ms()
     probe_ms, probe_pick = sess.probe()
+    dense1, _ = sess.counters()
+    dense_per_launch = (dense1 - dense0) / K
     if dist is not None:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -158,11 +161,15 @@ def main():
     errhist_final = float(res["errHist"][-1]) if len(res["errHist"]) else None
 
     # algorithmic bytes of the dominant kernel (fused update K5), per launch,
-    # on this rank's shard: reads D,Y_L,E,Y_O + writes E,Y_L,Y_O,T (8 N-streams;
-    # O is rebuilt on demand) + W (R * n1 * n2 doubles)
+    # on this rank's shard: reads D, Y_L, Y_O + writes Y_L, Y_O,
+    # T (6 N-streams of 8 B; O is rebuilt on demand), E in compact form (one
+    # 256 B slot per 256-element tile read and written = 2 B per element),
+    # 4 KB per tile stored densely (more than 28 nonzeros; read next launch),
+    # and W (R * n1 * n2 doubles)
     nl = i1 - i0
     N_local = nl * n * n
-    k5_bytes = (8 * N_local + r * r * nl * n) * 8
+    k5_bytes = int(6 * N_local * 8 + 2 * tiles_per_launch * 256 + dense_per_launch * 4096
+                   + r * r * nl * n * 8)
     k5_ms = km["fused_update"]
     achieved = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
     traffic, traffic_src = pmc_traffic()
@@ -199,7 +206,9 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": k5_bytes},
+                         "algorithmic_bytes_per_launch": k5_bytes,
+                         "e_dense_tiles_per_launch": dense_per_launch,
+                         "e_tiles_per_launch": tiles_per_launch},
             "cpu_baseline": cpu,
             # candidate tensor pools timed with K5's access pattern at session
             # creation (rank 0), the fastest kept

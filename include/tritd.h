@@ -142,6 +142,11 @@ tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, 
  * the index kept.  *n = 1 when probing was skipped. */
 tritd_status tritd_session_probe(tritd_session* s, double* ms, int32_t cap, int32_t* n,
                                  int32_t* picked);
+/* Compact-E counters: E tiles stored densely (more than 28
+ * nonzeros of 256) summed over all fused-update launches so far, and the
+ * number of tiles one launch covers. */
+tritd_status tritd_session_counters(tritd_session* s, int64_t* dense_tiles_total,
+                                    int64_t* tiles_per_launch);
 void tritd_session_destroy(tritd_session* s);
 
 /* ---------------------------------------------------------------------------

@@ -7,7 +7,7 @@
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r01}
-ALG=${2:-8724152320}   # K5 algorithmic bytes per launch
+ALG=${2:-6845104128}   # K5 algorithmic bytes per launch at 512^3 r=8 without dense E tiles
 O=gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- \

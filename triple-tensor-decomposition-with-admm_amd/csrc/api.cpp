@@ -221,6 +221,14 @@ tritd_status tritd_session_probe(tritd_session* s, double* ms, int32_t cap, int3
     });
 }
 
+tritd_status tritd_session_counters(tritd_session* s, int64_t* dense_tiles_total,
+                                    int64_t* tiles_per_launch) {
+    return guarded([&] {
+        need(s, "session");
+        reinterpret_cast<Session*>(s)->counters(dense_tiles_total, tiles_per_launch);
+    });
+}
+
 void tritd_session_destroy(tritd_session* s) { delete reinterpret_cast<Session*>(s); }
 
 tritd_status tritd_comm_unique_id(void* id128) {

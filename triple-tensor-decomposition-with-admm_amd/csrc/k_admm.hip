@@ -118,7 +118,8 @@ __device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
 // Branch-free: a branch here makes the compiler's vmcnt waits drain the
 // prefetch.
 __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, double* cs, double* CE,
-                                          int64_t sb, d2v* E2, int64_t o) {
+                                          int64_t sb, d2v* E2, int64_t o,
+                                          unsigned long long* dense_tiles) {
     uint64_t nz[4];
     int cnt = 0;
 #pragma unroll
@@ -154,6 +155,7 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
     if (dense) {
         E2[o] = d2v{En[0], En[1]};
         E2[o + 64] = d2v{En[2], En[3]};
+        if (lane == 0) atomicAdd(dense_tiles, 1ull);
     }
     const __amdgpu_buffer_rsrc_t rs = wave_rsrc(CE + sb, CE_SLOT * 8);
     const double sv = (dense && l >= 4) ? 0.0 : v;
@@ -363,7 +365,7 @@ void k5_fused(K5Args a) {
                 st2(YLn2, YL2 + o + 64 * p);
                 st2(YOn2, YO2 + o + 64 * p);
             }
-            ce_encode(En, lane, cs, a.CE, (tb >> 8) * CE_SLOT, E2, o);
+            ce_encode(En, lane, cs, a.CE, (tb >> 8) * CE_SLOT, E2, o, a.dense_tiles);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
         if (K5_EXP & 8) {

@@ -28,6 +28,7 @@ struct K5Args {
     int64_t n1p, n2, n3p, plane, tiles, ntt;
     IterScalars s;
     const int* stop;
+    unsigned long long* dense_tiles;  // running count of E tiles stored densely
     int rot;  // rotate each workgroup's t-walk (0 = natural order)
 };
 int k5_grid(const Geom& g);

@@ -159,8 +159,8 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     errO_.alloc(mi);
     for (DBuf* b : {&errHist_, &errL_, &errO_, &red1_, &red2_, &red3_})
         TRITD_HIP(hipMemsetAsync(b->p, 0, b->n * sizeof(double), st_));
-    TRITD_HIP(hipMalloc(&ctrl_, 4 * sizeof(int)));
-    TRITD_HIP(hipMemsetAsync(ctrl_, 0, 4 * sizeof(int), st_));
+    TRITD_HIP(hipMalloc(&ctrl_, 4 * sizeof(int) + sizeof(unsigned long long)));
+    TRITD_HIP(hipMemsetAsync(ctrl_, 0, 4 * sizeof(int) + sizeof(unsigned long long), st_));
 
     // D -> tile-major device layout (one-off)
     if (g_.n1l > 0 && n2 * n3 > 0) {
@@ -199,6 +199,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     a.ntt = g_.ntt;
     a.s = scalars(1);
     a.stop = ctrl_;
+    a.dense_tiles = dense_tiles();
     a.rot = rot_;
     if (o_.maxIter > 0) launch_k5(g_, a, /*prologue=*/true, st_);
     if (overlap_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
@@ -370,6 +371,7 @@ void Session::launch_k5_full(int k, bool fused_finish) {
     a.ntt = g_.ntt;
     a.s = scalars(k);
     a.stop = ctrl_;
+    a.dense_tiles = dense_tiles();
     a.rot = rot_;
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
     launch_k5(g_, a, /*prologue=*/false, st_);
@@ -553,6 +555,15 @@ void Session::get(double* A, double* B, double* C, double* O, double* E, int64_t
     if (errHist && done > 0)
         TRITD_HIP(hipMemcpy(errHist, errHist_.p, (size_t)done * sizeof(double), hipMemcpyDeviceToHost));
     if (iters) *iters = done;
+}
+
+void Session::counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch) {
+    TRITD_HIP(hipSetDevice(device_));
+    unsigned long long h = 0;
+    TRITD_HIP(hipStreamSynchronize(st_));
+    TRITD_HIP(hipMemcpy(&h, dense_tiles(), sizeof h, hipMemcpyDeviceToHost));
+    if (dense_tiles_total) *dense_tiles_total = (int64_t)h;
+    if (tiles_per_launch) *tiles_per_launch = g_.Ntm / 256;
 }
 
 void Session::rre_parts(const double* dX, int64_t ldX, double* num, double* den) {

@@ -54,6 +54,7 @@ class Session {
     void get(double* A, double* B, double* C, double* O, double* E, int64_t ldOE, double* errHist,
              int* iters);
     void rre_parts(const double* dX, int64_t ldX, double* num, double* den);
+    void counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch);
     void set_timing(bool on);
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
     const std::vector<double>& probe_ms() const { return probe_ms_; }
@@ -114,7 +115,10 @@ class Session {
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;
     DBuf errHist_, errL_, errO_;
-    int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag
+    int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag, [4..5] u64 dense E tiles
+    unsigned long long* dense_tiles() const {
+        return reinterpret_cast<unsigned long long*>(ctrl_ + 4);
+    }
 
     bool timing_ = false;
     std::vector<hipEvent_t> ev_;  // per timed iteration: 6 events

@@ -266,6 +266,12 @@ class Session:
         check(lib.tritd_session_probe(self._s, ms, 16, C.byref(n), C.byref(k)))
         return [ms[i] for i in range(min(n.value, 16))], k.value
 
+    def counters(self):
+        """(E tiles stored densely over all fused-update launches, tiles per launch)"""
+        a, b = _lib.i64(0), _lib.i64(0)
+        check(lib.tritd_session_counters(self._s, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def set_timing(self, on=True):
         check(lib.tritd_session_set_timing(self._s, int(bool(on))))
 
