@@ -94,6 +94,14 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
                             const tritd_opts* opts, const double* A0, const double* B0,
                             const double* C0, double* A, double* B, double* C, double* O,
                             double* E, double* errHist, int32_t* iters, int32_t device);
+/* The same for D of MATLAB class single: O, E and
+ * every array derived from D are single; A, B, C, errHist double (holding
+ * the single-rounded values MATLAB's class rules produce).  r <= 16.
+ * MATLAB: the wrapper passes single(D) here, mxSINGLE_CLASS outputs. */
+tritd_status tritd_admm_f32(const float* D, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                            const tritd_opts* opts, const double* A0, const double* B0,
+                            const double* C0, double* A, double* B, double* C, float* O, float* E,
+                            double* errHist, int32_t* iters, int32_t device);
 
 /* ---------------------------------------------------------------------------
  * Sessions: the device-resident ADMM loop, steppable (bench), shardable
@@ -104,14 +112,15 @@ typedef struct tritd_session tritd_session;
 typedef struct tritd_comm tritd_comm;
 
 enum {
-    TRITD_SESSION_D_ON_DEVICE = 1 /* D is a device pointer on `device` */
+    TRITD_SESSION_D_ON_DEVICE = 1, /* D is a device pointer on `device` */
+    TRITD_SESSION_F32 = 2          /* D is float (class single): the fp32 data path */
 };
 
-/* D points at D(i0,0,0); consecutive (j,t) fibres are ldD elements apart
+/* D points at D(i0,0,0) (double, or float with TRITD_SESSION_F32); consecutive (j,t) fibres are ldD elements apart
  * (ldD = n1 for a full column-major tensor).  A0 is the FULL (n1,r,r)
  * initial A (rows i0..i1-1 are used); B0, C0 are full.  comm = NULL for a
  * single process/GPU. */
-tritd_status tritd_session_create(tritd_session** out, int32_t device, const double* D, int64_t ldD,
+tritd_status tritd_session_create(tritd_session** out, int32_t device, const void* D, int64_t ldD,
                                   int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1,
                                   int32_t r, const tritd_opts* opts, const double* A0,
                                   const double* B0, const double* C0, tritd_comm* comm,
@@ -132,6 +141,11 @@ tritd_status tritd_session_get(tritd_session* s, double* A, double* B, double* C
  * (Combine across ranks, then RRE = sqrt(num/den).) */
 tritd_status tritd_session_rre_parts(tritd_session* s, const double* dX, int64_t ldX, double* num,
                                      double* den);
+/* fp32 sessions (TRITD_SESSION_F32): O, E and the reference tensor are float. */
+tritd_status tritd_session_get_f32(tritd_session* s, double* A, double* B, double* C, float* O,
+                                   float* E, int64_t ldOE, double* errHist, int32_t* iters);
+tritd_status tritd_session_rre_parts_f32(tritd_session* s, const float* dX, int64_t ldX,
+                                         double* num, double* den);
 /* Kernel-level timing of the dominant kernels over the last run (ms per
  * launch, HIP events on the session stream; 0 when timing is disabled). */
 tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable);

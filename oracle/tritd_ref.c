@@ -374,5 +374,133 @@ int tritd_ref_admm(const double* D, idx n1, idx n2, idx n3, int r, const double*
     return k;
 }
 
+
+/* ------------------------------------------------- single-precision D */
+/* triple_decomp_ADMM with D of class single, following MATLAB's class rules
+ * (SURVEY.md §8a row 1): every array derived from D (T, O, E, Y_L, Y_O,
+ * residuals) is single and each statement of :33,:41-53 is evaluated in
+ * single, with the double scalars (1/mu, mu, lambda/mu, mu+mu) converted to
+ * single where they meet a single array; L = triple_product(A,B,C) is double
+ * (A, B, C are double) and converted to single where it meets D (:41,:50);
+ * X_k*F' (single * double) is a single result: here accumulated in double and
+ * rounded to single once (MATLAB's sgemm accumulates in single: a difference
+ * at single rounding level); Grams and pinv are double; (X*F')*pinv(G) is
+ * single again and reshaped into the double A/B/C (reshape_*: zeros() then
+ * element assignment).  norm() of a single array is single: squares summed
+ * in double, root rounded to single; errHist(k) = single(eL + eO) stored in
+ * the double errHist.  The zero initial O, E, Y_L, Y_O are exact in either
+ * class, so iteration 1 already runs in single. */
+static void round_to_single(double* x, idx n) {
+    for (idx e = 0; e < n; ++e) x[e] = (double)(float)x[e];
+}
+
+int tritd_ref_admm_f32(const float* D, idx n1, idx n2, idx n3, int r, const double* opts7,
+                       const double* A0, const double* B0, const double* C0, double* A, double* B,
+                       double* C, float* O, float* E, double* errHist, int max_iters_override) {
+    const int R = r * r;
+    const idx N = n1 * n2 * n3;
+    double muL = opts7[0], rhoL = opts7[1], muL_max = opts7[0] * 1e6;
+    double muO = opts7[0], rhoO = opts7[1], muO_max = opts7[0] * 1e6;
+    const double lambda = opts7[2], lambda2 = opts7[3];
+    int maxIter = (int)opts7[4];
+    const double tol = opts7[5];
+    const int disp = opts7[6] != 0;
+    if (max_iters_override > 0 && max_iters_override < maxIter) maxIter = max_iters_override;
+
+    memcpy(A, A0, (size_t)(n1 * R) * 8);
+    memcpy(B, B0, (size_t)(R * n2) * 8);
+    memcpy(C, C0, (size_t)(R * n3) * 8);
+    float *YL = (float*)malloc((size_t)N * 4), *YO = (float*)malloc((size_t)N * 4);
+    double *Td = dalloc(N), *L = dalloc(N), *X2 = dalloc(N), *X3 = dalloc(N);
+    idx fmax_cols = n2 * n3;
+    if (n1 * n3 > fmax_cols) fmax_cols = n1 * n3;
+    if (n1 * n2 > fmax_cols) fmax_cols = n1 * n2;
+    double* F = dalloc((idx)R * fmax_cols);
+    double *G = dalloc((idx)R * R), *Pi = dalloc((idx)R * R);
+    idx nmax = n1 > n2 ? n1 : n2;
+    if (n3 > nmax) nmax = n3;
+    double *Mk = dalloc(nmax * R), *Yk = dalloc(nmax * R);
+#pragma omp parallel for schedule(static)
+    for (idx e = 0; e < N; ++e) O[e] = E[e] = YL[e] = YO[e] = 0.0f;
+
+    double ss = 0;
+#pragma omp parallel for reduction(+ : ss) schedule(static)
+    for (idx e = 0; e < N; ++e) ss += (double)D[e] * (double)D[e];
+    const float normD = (float)sqrt(ss);
+
+    int k = 0;
+    for (k = 1; k <= maxIter; ++k) {
+        const float invL = (float)(1.0 / muL), invO = (float)(1.0 / muO);
+#pragma omp parallel for schedule(static)
+        for (idx e = 0; e < N; ++e) {
+            const float t = (D[e] - O[e]) + invL * YL[e]; /* :33 in single */
+            Td[e] = (double)t;
+        }
+        /* update_A */
+        tritd_ref_build('F', B, C, n2, n3, r, F);
+        gram_ffT(F, R, n2 * n3, lambda2, G);
+        pinv_sym(G, R, Pi);
+        gemm_x_ft(Td, n1, n2 * n3, F, R, Mk);
+        round_to_single(Mk, n1 * R); /* X1*F.' : single */
+        small_mm(Mk, n1, R, Pi, A);
+        round_to_single(A, n1 * R); /* (..)*pinv(G) : single, assigned into double A */
+        /* update_B */
+        tritd_ref_unfold(Td, n1, n2, n3, 2, X2);
+        tritd_ref_build('G', A, C, n1, n3, r, F);
+        gram_ffT(F, R, n1 * n3, lambda2, G);
+        pinv_sym(G, R, Pi);
+        gemm_x_ft(X2, n2, n1 * n3, F, R, Mk);
+        round_to_single(Mk, n2 * R);
+        small_mm(Mk, n2, R, Pi, Yk);
+        round_to_single(Yk, n2 * R);
+        reshape_B_from_B2(Yk, n2, r, B);
+        /* update_C */
+        tritd_ref_unfold(Td, n1, n2, n3, 3, X3);
+        tritd_ref_build('H', A, B, n1, n2, r, F);
+        gram_ffT(F, R, n1 * n2, 1e-9, G);
+        pinv_sym(G, R, Pi);
+        gemm_x_ft(X3, n3, n1 * n2, F, R, Mk);
+        round_to_single(Mk, n3 * R);
+        small_mm(Mk, n3, R, Pi, Yk);
+        round_to_single(Yk, n3 * R);
+        reshape_C_from_C3(Yk, n3, r, C);
+        /* L = triple_product(A,B,C), double */
+        tritd_ref_build('F', B, C, n2, n3, r, F);
+        triple_product_F(A, n1, R, F, n2 * n3, L);
+
+        const float fmuL = (float)muL, fmuO = (float)muO;
+        const float den = (float)(muL + muO), thr = (float)(lambda / muO);
+        double sL = 0, sO = 0;
+#pragma omp parallel for reduction(+ : sL, sO) schedule(static)
+        for (idx e = 0; e < N; ++e) {
+            const float d = D[e], Lf = (float)L[e], yl = YL[e], yo = YO[e];
+            const float R1 = (d - Lf) + invL * yl;                             /* :41 */
+            const float R2 = E[e] - invO * yo;                                 /* :42 */
+            const float On = (fmuL * R1 + fmuO * R2) / den;                    /* :43 */
+            const float R3 = On + invO * yo;                                   /* :46 */
+            const float sg = R3 > 0 ? 1.0f : (R3 < 0 ? -1.0f : (R3 == 0 ? 0.0f : R3));
+            const float En = sg * fmaxf(fabsf(R3) - thr, 0.0f);                /* :47 */
+            const float rL = (d - Lf) - On;                                    /* :50 */
+            const float rO = On - En;                                          /* :51 */
+            YL[e] = yl + fmuL * rL;                                            /* :52 */
+            YO[e] = yo + fmuO * rO;                                            /* :53 */
+            O[e] = On;
+            E[e] = En;
+            sL += (double)rL * (double)rL;
+            sO += (double)rO * (double)rO;
+        }
+        muL = fmin(muL * rhoL, muL_max);
+        muO = fmin(muO * rhoO, muO_max);
+        const float eL = (float)sqrt(sL) / normD, eO = (float)sqrt(sO) / normD;
+        errHist[k - 1] = (double)(eL + eO); /* :59 (single, stored into double) */
+        if (disp && k % 10 == 0) printf("Iter %d, errL=%.2e, errO=%.2e\n", k, eL, eO);
+        if (k > 1 && fabs(errHist[k - 1] - errHist[k - 2]) < tol * errHist[k - 2]) break;
+    }
+    if (k > maxIter) k = maxIter;
+    free(YL); free(YO); free(Td); free(L); free(X2); free(X3); free(F);
+    free(G); free(Pi); free(Mk); free(Yk);
+    return k;
+}
+
 int tritd_ref_threads(void) { return omp_get_max_threads(); }
 void tritd_ref_set_threads(int n) { omp_set_num_threads(n); }

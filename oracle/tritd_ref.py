@@ -18,6 +18,8 @@ def load():
     lib.tritd_ref_admm.restype = C.c_int
     lib.tritd_ref_admm.argtypes = [vp, i64, i64, i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                    vp, C.c_int]
+    lib.tritd_ref_admm_f32.restype = C.c_int
+    lib.tritd_ref_admm_f32.argtypes = lib.tritd_ref_admm.argtypes
     lib.tritd_ref_triple_product.argtypes = [vp, vp, vp, i64, i64, i64, C.c_int, vp]
     lib.tritd_ref_unfold.argtypes = [vp, i64, i64, i64, C.c_int, vp]
     lib.tritd_ref_build.argtypes = [C.c_char, vp, vp, i64, i64, C.c_int, vp]
@@ -31,17 +33,21 @@ def _p(a):
 
 
 def admm(lib, D, r, opts, A0, B0, C0, max_iters=0):
-    D = np.asfortranarray(D, dtype=np.float64)
+    """C restatement; D of dtype float32 selects the MATLAB-single path."""
+    single = np.asarray(D).dtype == np.float32
+    D = np.asfortranarray(D, dtype=np.float32 if single else np.float64)
     n1, n2, n3 = D.shape
     o = np.array([opts["mu"], opts["rho"], opts["lambda"], opts["lambda2"], opts["maxIter"],
                   opts["tol"], opts["disp"]], dtype=np.float64)
     A = np.zeros((n1, r, r), order="F")
     B = np.zeros((r, n2, r), order="F")
     Cc = np.zeros((r, r, n3), order="F")
-    O = np.zeros((n1, n2, n3), order="F")
-    E = np.zeros((n1, n2, n3), order="F")
+    dt = np.float32 if single else np.float64
+    O = np.zeros((n1, n2, n3), order="F", dtype=dt)
+    E = np.zeros((n1, n2, n3), order="F", dtype=dt)
     eh = np.zeros(max(int(opts["maxIter"]), 1))
     A0, B0, C0 = (np.asfortranarray(x, dtype=np.float64) for x in (A0, B0, C0))
-    k = lib.tritd_ref_admm(_p(D), n1, n2, n3, r, _p(o), _p(A0), _p(B0), _p(C0), _p(A), _p(B),
+    fn = lib.tritd_ref_admm_f32 if single else lib.tritd_ref_admm
+    k = fn(_p(D), n1, n2, n3, r, _p(o), _p(A0), _p(B0), _p(C0), _p(A), _p(B),
                            _p(Cc), _p(O), _p(E), _p(eh), int(max_iters))
     return A, B, Cc, O, eh[:k].copy(), E, k

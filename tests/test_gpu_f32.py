@@ -1,0 +1,124 @@
+"""fp32 data path (D of MATLAB class single; SURVEY.md §8a row 1, §8b
+tritd_admm_f32, §8d config 5) against the single-class C restatement
+(oracle/tritd_ref.c: tritd_ref_admm_f32) on the same inputs.
+
+Tolerances (stated here): both sides round to single at the
+same statements but accumulate their GEMMs in different orders (the oracle
+in double then rounded once, the GPU in single on MFMA), so the iterates
+agree at single-precision level on well-conditioned problems (n_k >= R):
+relative Frobenius error of L = triple_product(A,B,C), O, E <= 2e-5 and the
+same iteration count.  errHist is compared with an absolute floor of
+1e-4 * errHist(1): once the residuals reach single-precision noise their
+norms are noise on both sides.  Ill-conditioned Grams (n_k < R) amplify
+single rounding by their condition number on any implementation and are
+not used for parity.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+
+@pytest.fixture(scope="module")
+def tritd():
+    import tritd as t
+    assert t.device_count() > 0
+    return t
+
+
+@pytest.fixture(scope="module")
+def cref():
+    import os
+    import subprocess
+    import tritd_oracle
+    here = os.path.dirname(os.path.abspath(tritd_oracle.__file__))
+    subprocess.run(["make", "-C", here], check=True, capture_output=True)
+    import tritd_ref
+    return tritd_ref, tritd_ref.load()
+
+
+def _compare(tritd, cref, D, r, opts, A0, B0, C0, tol=TOL):
+    import tritd_oracle as orc
+    mod, lib = cref
+    ref = mod.admm(lib, D, r, opts, A0, B0, C0)
+    A, B, C, O, eh, E, k = tritd.triple_decomp_ADMM(D, r, opts, A0, B0, C0, return_E=True,
+                                                    return_iters=True)
+    assert O.dtype == np.float32 and E.dtype == np.float32 and A.dtype == np.float64
+    assert k == ref[6]
+    L = orc.triple_product(A, B, C)
+    Lr = orc.triple_product(ref[0], ref[1], ref[2])
+    assert rel(L, Lr) <= tol
+    assert rel(O.astype(np.float64), ref[3].astype(np.float64)) <= tol
+    if np.any(ref[5]):
+        assert rel(E.astype(np.float64), ref[5].astype(np.float64)) <= tol
+    else:
+        assert not np.any(E)
+    np.testing.assert_allclose(eh, ref[4], rtol=1e-3, atol=1e-4 * ref[4][0])
+    return E
+
+
+@pytest.mark.parametrize("shape,r,iters", [((24, 20, 18), 3, 30), ((80, 64, 96), 5, 40),
+                                           ((128, 16, 64), 4, 40), ((96, 80, 72), 8, 30)])
+def test_f32_vs_c_oracle(tritd, cref, shape, r, iters):
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(*shape, r, seed=2, init_seed=7)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=iters)
+    _compare(tritd, cref, d["D"].astype(np.float32), r, opts, d["A0"], d["B0"], d["C0"])
+
+
+@pytest.mark.parametrize("case", ["mixed_tiles", "all_dense"])
+def test_f32_compact_e_overflow_tiles(tritd, cref, case):
+    """Compact E in fp32: 64-word slots, more than 56 nonzeros of a 256-element
+    tile go dense (k_admm32.hip)."""
+    from tritd import synth
+    n1, n2, n3, r = 64, 40, 64, 3
+    d = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=11, init_seed=5)
+    D = d["D"].copy(order="F")
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=30)
+    if case == "mixed_tiles":
+        rng = np.random.default_rng(3)
+        D[:16, :7, :40] += 8.0 * rng.standard_normal((16, 7, 40))
+    else:
+        opts["lambda"] = 1e-6
+    E = _compare(tritd, cref, D.astype(np.float32), r, opts, d["A0"], d["B0"], d["C0"])
+    nnz = np.count_nonzero(E) / E.size
+    assert (nnz > 0.5) if case == "all_dense" else (0.02 < nnz < 0.5)
+
+
+def test_f32_stepping_is_deterministic(tritd):
+    from tritd import synth
+    n, r = 64, 4
+    d = synth.low_rank_plus_outliers(n, n, n, r, seed=0)
+    D = d["D"].astype(np.float32)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
+
+    def session():
+        return tritd.Session(r, opts, d["A0"], d["B0"], d["C0"], n1=n, n2=n, n3=n, D=D, device=0)
+
+    s1 = session()
+    s1.run(7)
+    s1.run(8)
+    r1 = s1.get()
+    s1.close()
+    s2 = session()
+    s2.run(15)
+    r2 = s2.get()
+    s2.close()
+    assert r1["k"] == r2["k"] == 15
+    assert r1["O"].dtype == np.float32
+    for key in ("A", "B", "C", "O", "E", "errHist"):
+        np.testing.assert_array_equal(r1[key], r2[key])
+
+
+def test_f32_zero_iterations(tritd):
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(20, 18, 16, 2, seed=0)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=0)
+    A, B, C, O, eh = tritd.triple_decomp_ADMM(d["D"].astype(np.float32), 2, opts, d["A0"],
+                                              d["B0"], d["C0"])
+    assert len(eh) == 0 and not np.any(O) and O.dtype == np.float32
+    np.testing.assert_array_equal(A, d["A0"])

@@ -58,10 +58,11 @@ tritd_opts normalized(const tritd_opts* o) {
     return c;
 }
 
-void check_dims(int64_t n1, int64_t n2, int64_t n3, int32_t r) {
+void check_dims(int64_t n1, int64_t n2, int64_t n3, int32_t r, bool f32 = false) {
     if (n1 <= 0 || n2 <= 0 || n3 <= 0) throw Error(TRITD_ERR_ARG, "tensor dimensions must be positive");
     if (r <= 0) throw Error(TRITD_ERR_ARG, "rank r must be positive");
-    if (r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "fp64 path supports r <= 8 (R = r^2 <= 64)");
+    if (!f32 && r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "fp64 path supports r <= 8 (R = r^2 <= 64)");
+    if (f32 && r > 16) throw Error(TRITD_ERR_UNSUPPORTED, "fp32 path supports r <= 16 (R = r^2 <= 256)");
 }
 
 void need(const void* p, const char* what) {
@@ -99,7 +100,7 @@ void emit_line(const char* line) {
 
 extern "C" {
 
-const char* tritd_version(void) { return "tritd-mi355x 0.1.0 (gfx950, fp64)"; }
+const char* tritd_version(void) { return "tritd-mi355x 0.2.0 (gfx950, fp64 r<=8, fp32 r<=16)"; }
 const char* tritd_last_error(void) { return g_last_error.c_str(); }
 
 void tritd_set_print_callback(tritd_print_fn fn, void* user) {
@@ -135,7 +136,26 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
     });
 }
 
-tritd_status tritd_session_create(tritd_session** out, int32_t device, const double* D, int64_t ldD,
+tritd_status tritd_admm_f32(const float* D, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                            const tritd_opts* opts, const double* A0, const double* B0,
+                            const double* C0, double* A, double* B, double* C, float* O, float* E,
+                            double* errHist, int32_t* iters, int32_t device) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        check_opts(opts);
+        check_dims(n1, n2, n3, r, true);
+        need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        const int dev = pick_device(device);
+        const tritd_opts o = normalized(opts);
+        Session s(dev, D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, TRITD_SESSION_F32);
+        s.run(o.maxIter);
+        int k = 0;
+        s.get(A, B, C, O, E, n1, errHist, &k);
+        if (iters) *iters = k;
+    });
+}
+
+tritd_status tritd_session_create(tritd_session** out, int32_t device, const void* D, int64_t ldD,
                                   int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1,
                                   int32_t r, const tritd_opts* opts, const double* A0,
                                   const double* B0, const double* C0, tritd_comm* comm,
@@ -144,7 +164,7 @@ tritd_status tritd_session_create(tritd_session** out, int32_t device, const dou
         need(out, "out");
         *out = nullptr;
         check_opts(opts);
-        check_dims(n1, n2, n3, r);
+        check_dims(n1, n2, n3, r, (flags & TRITD_SESSION_F32) != 0);
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
         if (i0 < 0 || i1 > n1 || i0 >= i1) throw Error(TRITD_ERR_ARG, "bad shard range");
         if (ldD < i1 - i0) throw Error(TRITD_ERR_ARG, "ldD smaller than the shard");
@@ -177,6 +197,20 @@ tritd_status tritd_session_get(tritd_session* s, double* A, double* B, double* C
     return guarded([&] {
         need(s, "session");
         auto* S = reinterpret_cast<Session*>(s);
+        if (S->is_f32()) throw Error(TRITD_ERR_ARG, "fp32 session: use tritd_session_get_f32");
+        if ((O || E) && ldOE < S->geom().n1l) throw Error(TRITD_ERR_ARG, "ldOE smaller than the shard");
+        int k = 0;
+        S->get(A, B, C, O, E, ldOE, errHist, &k);
+        if (iters) *iters = k;
+    });
+}
+
+tritd_status tritd_session_get_f32(tritd_session* s, double* A, double* B, double* C, float* O,
+                                   float* E, int64_t ldOE, double* errHist, int32_t* iters) {
+    return guarded([&] {
+        need(s, "session");
+        auto* S = reinterpret_cast<Session*>(s);
+        if (!S->is_f32()) throw Error(TRITD_ERR_ARG, "fp64 session: use tritd_session_get");
         if ((O || E) && ldOE < S->geom().n1l) throw Error(TRITD_ERR_ARG, "ldOE smaller than the shard");
         int k = 0;
         S->get(A, B, C, O, E, ldOE, errHist, &k);
@@ -188,7 +222,19 @@ tritd_status tritd_session_rre_parts(tritd_session* s, const double* dX, int64_t
                                      double* den) {
     return guarded([&] {
         need(s, "session"); need(dX, "X"); need(num, "num"); need(den, "den");
-        reinterpret_cast<Session*>(s)->rre_parts(dX, ldX, num, den);
+        auto* S = reinterpret_cast<Session*>(s);
+        if (S->is_f32()) throw Error(TRITD_ERR_ARG, "fp32 session: use tritd_session_rre_parts_f32");
+        S->rre_parts(dX, ldX, num, den);
+    });
+}
+
+tritd_status tritd_session_rre_parts_f32(tritd_session* s, const float* dX, int64_t ldX,
+                                         double* num, double* den) {
+    return guarded([&] {
+        need(s, "session"); need(dX, "X"); need(num, "num"); need(den, "den");
+        auto* S = reinterpret_cast<Session*>(s);
+        if (!S->is_f32()) throw Error(TRITD_ERR_ARG, "fp64 session: use tritd_session_rre_parts");
+        S->rre_parts(dX, ldX, num, den);
     });
 }
 

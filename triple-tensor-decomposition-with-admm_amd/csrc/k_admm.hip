@@ -519,10 +519,18 @@ void launch_reduce_pairs(const double* partial, int n, double* out, const int* s
 
 // ctrl[0] = stop flag, ctrl[1] = iterations completed (k of :68)
 __device__ __forceinline__ void finish_body(const double* ss, double normD, int k, double tol,
-                                            double* errHist, double* errL, double* errO, int* ctrl) {
-    const double eL = sqrt(ss[0]) / normD;  // norm(resL(:))/normD
-    const double eO = sqrt(ss[1]) / normD;  // norm(resO(:))/normD
-    const double e = eL + eO;               // :59
+                                            double* errHist, double* errL, double* errO, int* ctrl,
+                                            int single) {
+    double eL = sqrt(ss[0]) / normD;  // norm(resL(:))/normD
+    double eO = sqrt(ss[1]) / normD;  // norm(resO(:))/normD
+    double e = eL + eO;               // :59
+    if (single) {  // single residuals: single norms, single quotients and sum
+        const float fL = (float)sqrt(ss[0]) / (float)normD;
+        const float fO = (float)sqrt(ss[1]) / (float)normD;
+        eL = fL;
+        eO = fO;
+        e = (double)(fL + fO);
+    }
     errHist[k - 1] = e;
     errL[k - 1] = eL;
     errO[k - 1] = eO;
@@ -531,15 +539,15 @@ __device__ __forceinline__ void finish_body(const double* ss, double normD, int 
 }
 
 __global__ void k_finish(const double* ss, double normD, int k, double tol, double* errHist,
-                         double* errL, double* errO, int* ctrl) {
+                         double* errL, double* errO, int* ctrl, int single) {
     if (ctrl[0]) return;
-    finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl);
+    finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl, single);
 }
 
 __global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict__ p, int n,
                                                        double normD, int k, double tol,
                                                        double* errHist, double* errL, double* errO,
-                                                       int* ctrl) {
+                                                       int* ctrl, int single) {
     if (ctrl[0]) return;
     __shared__ double sx[256], sy[256];
     double x = 0.0, y = 0.0;
@@ -559,21 +567,22 @@ __global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict_
     }
     if (threadIdx.x == 0) {
         const double ss[2] = {sx[0], sy[0]};
-        finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl);
+        finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl, single);
     }
 }
 
 void launch_reduce_finish(const double* partial, int n, double normD, int k, double tol,
-                          double* errHist, double* errL, double* errO, int* ctrl, hipStream_t st) {
+                          double* errHist, double* errL, double* errO, int* ctrl, bool single,
+                          hipStream_t st) {
     hipLaunchKernelGGL(k_reduce_finish, dim3(1), dim3(256), 0, st, partial, n, normD, k, tol,
-                       errHist, errL, errO, ctrl);
+                       errHist, errL, errO, ctrl, (int)single);
     TRITD_CHECK_LAUNCH();
 }
 
 void launch_finish(const double* ss, double normD, int k, double tol, double* errHist, double* errL,
-                   double* errO, int* ctrl, hipStream_t st) {
+                   double* errO, int* ctrl, bool single, hipStream_t st) {
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, ss, normD, k, tol, errHist, errL, errO,
-                       ctrl);
+                       ctrl, (int)single);
     TRITD_CHECK_LAUNCH();
 }
 

@@ -1,0 +1,558 @@
+// K5 for data of class single (fp32 path) and its companions.
+//
+// Same fused update as k_admm.hip (triple_decomp_ADMM.m:38-53, next :33,
+// W = T x3 C^), evaluated under MATLAB's class rules for a single D: every
+// elementwise statement in single with the double scalars rounded to single
+// (IterScalars32), L from v_mfma_f32_16x16x4_f32 (MATLAB: double L rounded to
+// single where it meets D), W in single.  RP in {16, 32, 48, 64, 128, 256}.
+//
+// fp32 tile layout (one 16 x 16 TM tile = 256 floats = 1 KB): lane l holds
+// the four consecutive t = 4*(l>>4) + r (r = 0..3) of row i = l & 15 at
+// floats 4l..4l+3 -- the C/D map of the f32 16x16 MFMA (row = 4*(lane>>4) +
+// reg, col = lane & 15), so a tile moves with ONE dwordx4 per lane.  T is
+// stored in the TX order of the mode-3 MFMA operand: lane l, slot s holds
+// T(ij = 4s + (l>>4), t = l & 15) at float 4l + s.
+//
+// Compact E (fp32): one 64-float (256 B) slot per tile, lane l holding word
+// l: words 0..7 are the four 64-bit ballot masks (mask w <=> register element
+// w of every lane), words 8..63 the nonzeros in (w, lane) order; more than 56
+// nonzeros -> the tile is stored densely in E and its masks are all ones.
+#include "kernels.h"
+
+namespace tritd {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+static constexpr int K5W = 4;
+constexpr int CE32_CAP = CE32_SLOT - 8;
+
+bool rp_supported32(int RP) {
+    return RP == 16 || RP == 32 || RP == 48 || RP == 64 || RP == 128 || RP == 256;
+}
+int padded_rank32(int R) {
+    if (R <= 64) return (int)round_up(R, 16);
+    return R <= 128 ? 128 : 256;
+}
+
+__device__ __forceinline__ f4 mfma32(float a, float b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float sign32(float x) {  // MATLAB sign, select-only
+    const float s = x == 0.0f ? 0.0f : __builtin_copysignf(1.0f, x);
+    return __builtin_isnan(x) ? x : s;
+}
+__device__ __forceinline__ int lanes_below32(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t ce32_word(float sv, int w) {
+    const int b = __float_as_int(sv);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(b, 2 * w);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(b, 2 * w + 1);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ bool ce32_is_dense(float sv) {
+    return (ce32_word(sv, 0) & ce32_word(sv, 1) & ce32_word(sv, 2) & ce32_word(sv, 3)) == ~0ull;
+}
+// this lane's 4 elements from its slot word sv; true for a dense tile
+__device__ __forceinline__ bool ce32_decode(float sv, int lane, float (&e)[4]) {
+    uint64_t m[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) m[w] = ce32_word(sv, w);
+    const int b = __float_as_int(sv);
+    int pre = 8;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int src = (pre + lanes_below32(m[w])) & 63;
+        const int v = __builtin_amdgcn_ds_bpermute(src << 2, b);
+        e[w] = ((m[w] >> lane) & 1) ? __int_as_float(v) : 0.0f;
+        pre += __builtin_popcountll(m[w]);
+    }
+    return (m[0] & m[1] & m[2] & m[3]) == ~0ull;
+}
+// store this lane's 4 elements as the tile's slot (every lane one word), or
+// densely (wave-uniform, rare) when they do not fit.  cs: 128-float per-wave
+// LDS image (slot + junk area for the zeros: no divergent branch)
+__device__ __forceinline__ void ce32_encode(const float (&En)[4], int lane, float* cs,
+                                            float* slot, f4* Etile,
+                                            unsigned long long* dense_tiles) {
+    uint64_t nz[4];
+    int cnt = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        nz[w] = __ballot(En[w] != 0.0f);
+        cnt += __builtin_popcountll(nz[w]);
+    }
+    const bool dense = cnt > CE32_CAP;
+    cs[lane < 8 ? 64 + lane : lane] = 0.0f;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    int pre = 8;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int bit = dense ? 0 : (int)((nz[w] >> lane) & 1);
+        const int at = pre + lanes_below32(nz[w]), away = 64 + lane;
+        cs[away + ((at - away) & -bit)] = En[w];
+        pre += __builtin_popcountll(nz[w]);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint64_t mw = dense ? ~0ull : nz[w];
+        cs[2 * w] = __int_as_float((int)(uint32_t)mw);
+        cs[2 * w + 1] = __int_as_float((int)(uint32_t)(mw >> 32));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const float v = cs[lane];
+    if (dense) {
+        Etile[lane] = f4{En[0], En[1], En[2], En[3]};
+        if (lane == 0) atomicAdd(dense_tiles, 1ull);
+    }
+    slot[lane] = (dense && lane >= 8) ? 0.0f : v;
+}
+
+// Register budget: two waves per SIMD up to RP = 128; at RP = 256 the L
+// operands (64) + W accumulators (64) + two tile sets (34) + C^ staging (16)
+// + L accumulators do not fit 256, and the kernel runs one wave per SIMD
+// (config 5 is MFMA-bound: 128 MFMAs per tile).
+template <int RP, bool PRO>
+__global__ __launch_bounds__(64 * K5W) __attribute__((amdgpu_waves_per_eu(RP >= 256 ? 1 : 2, 2)))
+void k5_f32(K5Args32 a) {
+    if (*a.stop) return;
+    constexpr int KS = RP / 4;    // MFMA K-steps of L
+    constexpr int MT = RP / 16;   // k-tiles of W
+    constexpr int LDC = RP + 4;   // [t][k] row stride: the 4 t-groups of a read fall in distinct banks
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int il = lane & 15;
+    const int tg = lane >> 4;
+    const int64_t tile = (int64_t)blockIdx.x * K5W + wid;
+    const bool active = tile < a.tiles;
+    const int64_t qper = a.n1p >> 4;
+    const int64_t j = active ? tile / qper : 0;
+    const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
+    const int64_t ntt = a.ntt;
+
+    __shared__ float sCT[2][RP * 16];   // [k][16]: L operand C^(t0 + l&15, 4s + (l>>4))
+    __shared__ float sC[2][16 * LDC];   // [t][k]:  W operand C^(t0 + 4(l>>4) + r, 16m + (l&15))
+    __shared__ float tsm[K5W][16 * 17]; // per-wave T transpose
+    __shared__ float csm[K5W][128];     // per-wave compact-E slot image
+    float* ts = tsm[wid];
+    float* cs = csm[wid];
+
+    // C^ slice of one t-tile: 16 rows x RP floats, loaded before the tile
+    // prefetch, written to LDS after the tile's compute (in-order vmcnt)
+    constexpr int SQ = 16 * RP / 4;
+    constexpr int NS = (SQ + 64 * K5W - 1) / (64 * K5W);
+    f4 sv[NS];
+    auto stage_load = [&](int64_t tt) {
+        const f4* src = reinterpret_cast<const f4*>(a.ChF + (tt << 4) * RP);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 64 * K5W;
+            if (SQ % (64 * K5W) == 0 || e < SQ) sv[q] = src[e];
+        }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 64 * K5W;
+            if (SQ % (64 * K5W) == 0 || e < SQ) {
+                const int row = (4 * e) / RP, k = (4 * e) % RP;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    sC[buf][row * LDC + k + c] = sv[q][c];
+                    sCT[buf][(k + c) * 16 + row] = sv[q][c];
+                }
+            }
+        }
+    };
+
+    float kr[KS];  // L operand KR(ij = l & 15, k = 4s + (l>>4)), single-rounded
+    if (!PRO) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + tg;
+            kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
+        }
+    }
+    f4 wacc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    double ssL = 0.0, ssO = 0.0;
+    const IterScalars32 sc = a.s;
+    const f4* D4 = reinterpret_cast<const f4*>(a.D);
+    f4* O4 = reinterpret_cast<f4*>(a.O);
+    f4* E4 = reinterpret_cast<f4*>(a.E);
+    f4* YL4 = reinterpret_cast<f4*>(a.YL);
+    f4* YO4 = reinterpret_cast<f4*>(a.YO);
+    f4* T4 = reinterpret_cast<f4*>(a.T);
+
+    // two register sets, unrolled by two (no cur = next copies); slots two
+    // tiles ahead so a dense tile is known when its batch is issued; the only
+    // branches are wave-uniform and rare (see k_admm.hip)
+    struct Regs {
+        f4 x[3];  // D, Y_L, Y_O (PRO: O)
+        f4 ed;    // dense E (overflowed tile only)
+        float ce; // this lane's slot word
+    };
+    auto tbase = [&](int64_t tt) { return tm_tile_base(tile, tt, ntt); };
+    auto load = [&](int64_t tt, Regs& nx) {
+        const int64_t o = (tbase(tt) >> 2) + lane;
+        nx.x[0] = D4[o];
+        nx.x[1] = YL4[o];
+        nx.x[2] = (PRO ? O4 : YO4)[o];
+    };
+    auto load_dense = [&](int64_t tt, Regs& nx) { nx.ed = E4[(tbase(tt) >> 2) + lane]; };
+    auto load_slot = [&](int64_t tt, float& ce) {
+        const int64_t t2 = tt < ntt ? tt : ntt - 1;
+        ce = a.CE[(tbase(t2) >> 8) * CE32_SLOT + lane];
+    };
+    auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+        const int64_t tb = tbase(tt);
+        const int64_t o = (tb >> 2) + lane;
+        if (pf) {
+            const bool dn1 = PRO ? false : ce32_is_dense(nx.ce);
+            stage_load(tt + 1);
+            load(tt + 1, nx);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!PRO && dn1) load_dense(tt + 1, nx);
+        }
+        float ev[4];
+        if (!PRO) {
+            const bool dn = ce32_decode(cx.ce, lane, ev);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
+            if (pf) load_slot(tt + 2, cx.ce);
+        }
+        const float* cT = sCT[buf];
+        const float* cR = sC[buf];
+        float tr[4];
+        if (PRO) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = cx.x[0][r], yl = cx.x[1][r], ov = cx.x[2][r];
+                tr[r] = (d - ov) + sc.invL * yl;  // :33
+            }
+        } else {
+            f4 lacc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                lacc[s & 3] = mfma32(cT[(4 * s + tg) * 16 + il], kr[s], lacc[s & 3]);
+            const f4 Lv = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
+            float En[4];
+            f4 YLn, YOn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = cx.x[0][r], yl = cx.x[1][r], yo = cx.x[2][r], e = ev[r];
+                const float L = Lv[r];
+                const float R1 = (d - L) + sc.invL * yl;               // :41
+                const float R2 = e - sc.invO * yo;                     // :42
+                const float On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
+                const float R3 = On + sc.invO * yo;                    // :46
+                const float Ev = sign32(R3) * fmaxf(fabsf(R3) - sc.thr, 0.0f);  // :47
+                const float rL = (d - L) - On;                         // :50
+                const float rO = On - Ev;                              // :51
+                const float yln = yl + sc.muL * rL;                    // :52
+                const float yon = yo + sc.muO * rO;                    // :53
+                tr[r] = (d - On) + sc.invL_next * yln;                 // :33 (k+1)
+                ssL += (double)rL * (double)rL;
+                ssO += (double)rO * (double)rO;
+                En[r] = Ev;
+                YLn[r] = yln;
+                YOn[r] = yon;
+            }
+            YL4[o] = YLn;
+            YO4[o] = YOn;
+            ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), a.dense_tiles);
+        }
+        // T -> TX order through the wave's LDS tile: ts[t][ij]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ts[(4 * tg + r) * 17 + il] = tr[r];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        f4 tv;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) tv[s] = ts[il * 17 + 4 * s + tg];
+        T4[o] = tv;
+        // W^T(k, ij) += sum_t C^(t,k) T(t,ij): K-step r covers t = 4(l>>4) + r
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                wacc[m] = mfma32(cR[(4 * tg + r) * LDC + 16 * m + il], tr[r], wacc[m]);
+        if (pf) stage_store(buf ^ 1);
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    Regs xa, xb;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) xa.x[q] = xb.x[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    xa.ed = xb.ed = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    xa.ce = xb.ce = 0.0f;
+    if (!PRO) {
+        load_slot(0, xa.ce);
+        load_slot(1, xb.ce);
+    }
+    load(0, xa);
+    if (!PRO && ce32_is_dense(xa.ce)) load_dense(0, xa);
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    int64_t tt = 0;
+    for (; tt + 2 < ntt; tt += 2) {
+        body(tt, 0, xa, xb, true);
+        body(tt + 1, 1, xb, xa, true);
+    }
+    if (tt + 1 < ntt) {
+        body(tt, 0, xa, xb, true);
+        body(tt + 1, 1, xb, xa, false);
+    } else {
+        body(tt, 0, xa, xb, false);
+    }
+    if (active) {
+        // W^T C/D layout (f32): row k = 16m + 4(l>>4) + rr, col ij = l & 15
+        const int64_t wbase = (tile << 4) + il;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                a.Wk[(int64_t)(16 * m + 4 * tg + rr) * a.plane + wbase] = wacc[m][rr];
+    }
+    if (!PRO) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            ssL += __shfl_xor(ssL, off);
+            ssO += __shfl_xor(ssO, off);
+        }
+        __shared__ double red[2][K5W];
+        if (lane == 0) {
+            red[0][wid] = ssL;
+            red[1][wid] = ssO;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double x = 0.0, y = 0.0;
+            for (int w = 0; w < K5W; ++w) {
+                x += red[0][w];
+                y += red[1][w];
+            }
+            a.partial[2 * blockIdx.x] = x;
+            a.partial[2 * blockIdx.x + 1] = y;
+        }
+    }
+}
+
+void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st) {
+    const dim3 grid(k5_grid(g)), block(64 * K5W);
+#define K5F_CASE(RPV)                                                        \
+    case RPV:                                                                \
+        if (prologue)                                                        \
+            hipLaunchKernelGGL((k5_f32<RPV, true>), grid, block, 0, st, a);  \
+        else                                                                 \
+            hipLaunchKernelGGL((k5_f32<RPV, false>), grid, block, 0, st, a); \
+        break;
+    switch (g.RP) {
+        K5F_CASE(16)
+        K5F_CASE(32)
+        K5F_CASE(48)
+        K5F_CASE(64)
+        K5F_CASE(128)
+        K5F_CASE(256)
+        default:
+            throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by the fp32 K5");
+    }
+#undef K5F_CASE
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// layout conversions, norms, O rebuild, compact-E expansion, placement probe
+// ---------------------------------------------------------------------------
+// float offset of (i, j, t) in the fp32 tile-major layout
+__host__ __device__ inline int64_t tm_offset32(int64_t i, int64_t j, int64_t t, int64_t n1p,
+                                               int64_t ntt) {
+    const int64_t g = (j * n1p + i) >> 4;
+    const int l = (int)((((t & 15) >> 2) << 4) | (i & 15));
+    return tm_tile_base(g, t >> 4, ntt) + 4 * l + (int)(t & 3);
+}
+
+__global__ __launch_bounds__(256) void k_to_tm32(const float* __restrict__ src, int64_t ld,
+                                                 int64_t n1l, int64_t n2, int64_t n3, int64_t n1p,
+                                                 int64_t ntt, int64_t Np, float* __restrict__ dst) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < Np; e += (int64_t)gridDim.x * 256) {
+        const int64_t blk = e >> 8;  // ((g/4)*ntt + tt)*4 + g%4
+        const int64_t q4 = blk >> 2, grp = q4 / ntt, tt = q4 - grp * ntt;
+        const int64_t g = grp * 4 + (blk & 3);
+        const int w = (int)(e & 255);
+        const int l = w >> 2, r = w & 3;
+        const int64_t t = 16 * tt + 4 * (l >> 4) + r;
+        const int64_t row = 16 * g + (l & 15);
+        const int64_t j = row / n1p, i = row - j * n1p;
+        dst[e] = (i < n1l && j < n2 && t < n3) ? src[(t * n2 + j) * ld + i] : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_from_tm32(const float* __restrict__ src, int64_t n1l,
+                                                   int64_t n2, int64_t n3, int64_t n1p, int64_t ntt,
+                                                   float* __restrict__ dst, int64_t ld) {
+    const int64_t total = n1l * n2 * n3;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * 256) {
+        const int64_t i = e % n1l, jt = e / n1l;
+        const int64_t j = jt % n2, t = jt / n2;
+        dst[(t * n2 + j) * ld + i] = src[tm_offset32(i, j, t, n1p, ntt)];
+    }
+}
+
+static unsigned grid_for32(int64_t n) {
+    int64_t b = cdiv(n, 256);
+    return (unsigned)(b > 16384 ? 16384 : (b < 1 ? 1 : b));
+}
+
+void launch_to_tm32(const Geom& g, const float* src, int64_t ld, float* dst, hipStream_t st) {
+    hipLaunchKernelGGL(k_to_tm32, dim3(grid_for32(g.Ntm)), dim3(256), 0, st, src, ld, g.n1l, g.n2,
+                       g.n3, g.n1p, g.ntt, g.Ntm, dst);
+    TRITD_CHECK_LAUNCH();
+}
+
+void launch_from_tm32(const Geom& g, const float* src, float* dst, int64_t ld, hipStream_t st) {
+    hipLaunchKernelGGL(k_from_tm32, dim3(grid_for32(g.n1l * g.n2 * g.n3)), dim3(256), 0, st, src,
+                       g.n1l, g.n2, g.n3, g.n1p, g.ntt, dst, ld);
+    TRITD_CHECK_LAUNCH();
+}
+
+// sum of squares in double (norm(D(:)) of a single D: the root is rounded to
+// single by the caller)
+__global__ __launch_bounds__(256) void k_sumsq32(const float* __restrict__ X, int64_t n,
+                                                 double* partial) {
+    double s = 0.0;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        const double x = (double)X[e];
+        s = fma(x, x, s);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+        partial[2 * blockIdx.x + 1] = 0.0;
+    }
+}
+
+void launch_sumsq32(const Geom& g, const float* X, double* partial, int nblocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_sumsq32, dim3(nblocks), dim3(256), 0, st, X, g.Ntm, partial);
+    TRITD_CHECK_LAUNCH();
+}
+
+// O_k from T_{k+1} = (D - O_k) + invL_next Y_L (the loop never stores O):
+// O = (D + invL_next Y_L) - T evaluated in double, rounded to single.  T is
+// in the TX order of the same tile: element (t = 4(l>>4)+r, i = l&15) sits
+// at TX lane ((i&3)<<4)|t, slot i>>2.
+__global__ __launch_bounds__(256) void k_o_fixup32(const float* __restrict__ D,
+                                                   const float* __restrict__ YL,
+                                                   const float* __restrict__ T, float invL_next,
+                                                   float* O, int64_t n) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        const int64_t base = e & ~(int64_t)255;
+        const int w = (int)(e & 255);
+        const int l = w >> 2, r = w & 3;
+        const int t = 4 * (l >> 4) + r, ii = l & 15;
+        const int tx = 4 * (((ii & 3) << 4) | t) + (ii >> 2);
+        const double v = ((double)D[e] + (double)invL_next * (double)YL[e]) - (double)T[base + tx];
+        O[e] = (float)v;
+    }
+}
+
+void launch_o_fixup32(const Geom& g, const float* D, const float* YL, const float* T,
+                      float invL_next, float* O, hipStream_t st) {
+    hipLaunchKernelGGL(k_o_fixup32, dim3(grid_for32(g.Ntm)), dim3(256), 0, st, D, YL, T, invL_next,
+                       O, g.Ntm);
+    TRITD_CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(256) void k_ce_expand32(const float* __restrict__ CE, float* E,
+                                                     int64_t ntiles) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= ntiles) return;
+    float e[4];
+    if (ce32_decode(CE[b * CE32_SLOT + lane], lane, e)) return;  // dense: E holds it
+    reinterpret_cast<f4*>(E)[b * 64 + lane] = f4{e[0], e[1], e[2], e[3]};
+}
+
+void launch_ce_expand32(const Geom& g, const float* CE, float* E, hipStream_t st) {
+    const int64_t ntiles = g.Ntm / 256;
+    hipLaunchKernelGGL(k_ce_expand32, dim3((unsigned)cdiv(ntiles, 4)), dim3(256), 0, st, CE, E,
+                       ntiles);
+    TRITD_CHECK_LAUNCH();
+}
+
+// K5's fp32 HBM pattern without arithmetic (placement probing)
+__global__ __launch_bounds__(256) void k_pool_probe32(float* D, float* YL, float* YO, float* T,
+                                                      float* CE, int64_t tiles4, int64_t ntt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= tiles4) return;
+    f4* P[4] = {reinterpret_cast<f4*>(D), reinterpret_cast<f4*>(YL), reinterpret_cast<f4*>(YO),
+                reinterpret_cast<f4*>(T)};
+    struct R {
+        f4 x[3];
+        float ce;
+    };
+    auto tb = [&](int64_t tt) { return tm_tile_base(tile, tt, ntt); };
+    auto load = [&](int64_t tt, R& n) {
+        const int64_t o = (tb(tt) >> 2) + lane;
+#pragma unroll
+        for (int f = 0; f < 3; ++f) n.x[f] = P[f][o];
+        n.ce = CE[(tb(tt) >> 8) * CE32_SLOT + lane];
+    };
+    auto body = [&](int64_t tt, R& c, R& n, bool pf) {
+        if (pf) {
+            load(tt + 1, n);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const int64_t o = (tb(tt) >> 2) + lane;
+        P[1][o] = c.x[0] + c.x[1];
+        P[2][o] = c.x[2] - c.x[1];
+        P[3][o] = c.x[0] - c.x[2];
+        CE[(tb(tt) >> 8) * CE32_SLOT + lane] = c.ce + 1.0f;
+    };
+    R xa, xb;
+    load(0, xa);
+    int64_t tt = 0;
+    for (; tt + 2 < ntt; tt += 2) {
+        body(tt, xa, xb, true);
+        body(tt + 1, xb, xa, true);
+    }
+    if (tt + 1 < ntt) {
+        body(tt, xa, xb, true);
+        body(tt + 1, xb, xa, false);
+    } else {
+        body(tt, xa, xb, false);
+    }
+}
+
+void launch_pool_probe32(const Geom& g, float* D, float* YL, float* YO, float* T, float* CE,
+                         hipStream_t st) {
+    hipLaunchKernelGGL(k_pool_probe32, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D, YL, YO,
+                       T, CE, g.tiles4, g.ntt);
+    TRITD_CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(256) void k_widen(const float* __restrict__ x, int64_t n, double* y) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+        y[e] = (double)x[e];
+}
+
+void launch_widen(const float* x, int64_t n, double* y, hipStream_t st) {
+    hipLaunchKernelGGL(k_widen, dim3(grid_for32(n)), dim3(256), 0, st, x, n, y);
+    TRITD_CHECK_LAUNCH();
+}
+
+}  // namespace tritd

@@ -1,0 +1,278 @@
+// Mode contractions of the fp32 data path (D of class single)
+// and the RP-general apply.
+//
+// MATLAB evaluates X_k*F' with X_k single as a single GEMM: M1, M2, M3 are
+// accumulated in single here (W and T are single); the factor operands
+// (A^ o B^, B^, A^) are the double factors rounded to single, as MATLAB
+// converts the double design matrix F/G/H when it meets a single X_k.
+#include "kernels.h"
+
+namespace tritd {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mfma32c(float a, float b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// M1(i,k) = sum_j W[k][j*n1p + i] * B^(j,k)   (single)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_m1_32(const float* __restrict__ Wk,
+                                               const double* __restrict__ Bh, float* M1,
+                                               int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                               const int* stop) {
+    if (*stop) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+    const int k = blockIdx.y;
+    float acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = 0.0f;
+    if (i < n1p) {
+        const float* wp = Wk + (int64_t)k * plane + i;
+        const double* bp = Bh + k;
+        int64_t j = w;
+        for (; j + 28 < n2; j += 32) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                acc[u] = fmaf(wp[(j + 4 * u) * n1p], (float)bp[(j + 4 * u) * RP], acc[u]);
+        }
+        for (; j < n2; j += 4) acc[0] = fmaf(wp[j * n1p], (float)bp[j * RP], acc[0]);
+    }
+    __shared__ float red[4][64];
+    red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (w == 0 && i < n1p) M1[i * RP + k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+void launch_m1_32(const Geom& g, const float* Wk, const double* Bh, float* M1, const int* stop,
+                  hipStream_t st) {
+    hipLaunchKernelGGL(k_m1_32, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(256), 0, st, Wk, Bh,
+                       M1, g.n1p, g.n2, g.plane, g.RP, stop);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// M2(j,k) = sum_i W[k][j*n1p + i] * A^(i,k)   (single sum, stored as double)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_m2_32(const float* __restrict__ Wk,
+                                               const double* __restrict__ AhT, double* M2,
+                                               int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                               const int* stop) {
+    if (*stop) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t j = blockIdx.x;
+    const int k = blockIdx.y * 4 + w;
+    if (k >= RP) return;
+    const float* wp = Wk + (int64_t)k * plane + j * n1p;
+    const double* ap = AhT + (int64_t)k * n1p;
+    float acc = 0.0f;
+    for (int64_t i = lane; i < n1p; i += 64) acc = fmaf(wp[i], (float)ap[i], acc);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) M2[j * RP + k] = (double)acc;
+}
+
+void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
+                  hipStream_t st) {
+    hipLaunchKernelGGL(k_m2_32, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
+                       AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// K2 (fp32) — M3(t,k) = sum_ij T(ij,t) A^(i,k) B^(j,k), any RP <= 256.
+// Workgroup = (t-group of 4 t-tiles, i-tile q, j-chunk); wave w owns t-tile
+// 4*tgrp + w and ALL RP columns (RP/16 f32x4 accumulators).  Walking j with
+// q fixed keeps the 16 A^ rows of the i-tile in registers; per j the
+// workgroup forms KR(ij,k) = single(A^(i,k) B^(j,k)) for the 16 ij of the
+// tile in LDS (double-buffered, one barrier per j) and each wave streams its
+// T tile (TX order: one dwordx4 per lane) as the B operand.  Per-workgroup
+// partials are summed in fixed order by k_m3_reduce32.
+// ---------------------------------------------------------------------------
+constexpr int M3W = 4;
+
+static int64_t m3_jchunks(const Geom& g) {
+    const int64_t ntg = cdiv(g.ntt, 4), qper = g.n1p >> 4;
+    int64_t jc = 2048 / (ntg * qper);
+    if (jc < 1) jc = 1;
+    if (jc > g.n2) jc = g.n2;
+    return jc;
+}
+
+int m3_parts32(const Geom& g) { return (int)((g.n1p >> 4) * m3_jchunks(g)); }
+
+template <int RP>
+__global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
+                                                    const double* __restrict__ Ah,
+                                                    const double* __restrict__ Bh, double* part,
+                                                    int64_t n1p, int64_t n2, int64_t n3p,
+                                                    int64_t ntt, int64_t jc, const int* stop) {
+    if (*stop) return;
+    constexpr int MT = RP / 16;
+    constexpr int KP = RP + 4;  // LDS row stride of KR (bank spread of the 4 ij rows a read touches)
+    constexpr int PER = 16 * RP / (64 * M3W);  // KR elements formed per thread per j
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int il = lane & 15, tg = lane >> 4;
+    const int64_t qper = n1p >> 4;
+    const int64_t tgrp = blockIdx.x / (qper * jc);
+    const int64_t rem = blockIdx.x - tgrp * qper * jc;
+    const int64_t q = rem / jc, c = rem - q * jc;
+    const int64_t ja = n2 * c / jc, jb = n2 * (c + 1) / jc;
+    const int64_t tt = tgrp * 4 + wid;
+    const bool tact = tt < ntt;
+    const int64_t ttl = tact ? tt : ntt - 1;  // inactive waves read a valid tile, store nothing
+
+    __shared__ float krs[2][16 * KP];
+    // this thread's KR elements: e = threadIdx.x + 256 u -> (row e / RP, col e % RP)
+    double ah[PER > 0 ? PER : 1];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int e = threadIdx.x + 64 * M3W * u;
+        ah[u] = Ah[(q * 16 + e / RP) * RP + e % RP];
+    }
+    auto form = [&](int64_t j, int buf) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 64 * M3W * u;
+            const int row = e / RP, k = e % RP;
+            krs[buf][row * KP + k] = (float)(ah[u] * Bh[j * RP + k]);
+        }
+    };
+    f4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const f4* T4 = reinterpret_cast<const f4*>(T);
+    auto tload = [&](int64_t j) { return T4[(tm_tile_base(j * qper + q, ttl, ntt) >> 2) + lane]; };
+
+    if (ja < jb) {
+        form(ja, 0);
+        f4 bnext = tload(ja);
+        __syncthreads();
+        for (int64_t j = ja; j < jb; ++j) {
+            const int buf = (int)((j - ja) & 1);
+            const f4 b = bnext;
+            if (j + 1 < jb) {
+                bnext = tload(j + 1);
+                form(j + 1, buf ^ 1);
+            }
+            const float* kr = krs[buf];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    acc[m] = mfma32c(kr[(4 * s + tg) * KP + 16 * m + il], b[s], acc[m]);
+            __syncthreads();
+        }
+    }
+    if (tact) {
+        // C/D (f32): row k = 16m + 4(l>>4) + rr, col t = 16 tt + (l & 15)
+        double* out = part + (q * jc + c) * n3p * RP;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                out[(tt * 16 + il) * RP + 16 * m + 4 * tg + rr] = (double)acc[m][rr];
+    }
+}
+
+// M3[e] = single(sum over parts in fixed order), stored as double
+__global__ __launch_bounds__(256) void k_m3_reduce32(const double* __restrict__ part, double* M3,
+                                                     int64_t count, int nparts, const int* stop) {
+    if (*stop) return;
+    const int lane = threadIdx.x & 63, qd = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+    double s = 0.0;
+    if (e < count)
+        for (int y = qd; y < nparts; y += 4) s += part[(int64_t)y * count + e];
+    __shared__ double red[4][64];
+    red[qd][lane] = s;
+    __syncthreads();
+    if (qd == 0 && e < count)
+        M3[e] = (double)(float)(((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+}
+
+void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double* Bh, double* part,
+                  double* M3, const int* stop, hipStream_t st) {
+    const int64_t jc = m3_jchunks(g), qper = g.n1p >> 4, ntg = cdiv(g.ntt, 4);
+    const dim3 grid((unsigned)(ntg * qper * jc)), block(64 * M3W);
+#define M3F_CASE(RPV)                                                                        \
+    case RPV:                                                                                \
+        hipLaunchKernelGGL(k_m3_32<RPV>, grid, block, 0, st, T, Ah, Bh, part, g.n1p, g.n2,   \
+                           g.n3p, g.ntt, jc, stop);                                          \
+        break;
+    switch (g.RP) {
+        M3F_CASE(16)
+        M3F_CASE(32)
+        M3F_CASE(48)
+        M3F_CASE(64)
+        M3F_CASE(128)
+        M3F_CASE(256)
+        default:
+            throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by the fp32 K2");
+    }
+#undef M3F_CASE
+    TRITD_CHECK_LAUNCH();
+    const int64_t count = g.n3p * g.RP;
+    hipLaunchKernelGGL(k_m3_reduce32, dim3((unsigned)cdiv(count, 64)), dim3(256), 0, st, part, M3,
+                       count, (int)(qper * jc), stop);
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Y = M * Ginv for any RP (the small-RP path of k_contract.hip stages Ginv in
+// LDS, which stops at RP = 64).  16 rows per block, M rows in LDS, Ginv read
+// from L2 column-wise (coalesced across the block's columns).
+// ---------------------------------------------------------------------------
+template <typename TM>
+__global__ __launch_bounds__(256) void k_apply_gen(const TM* __restrict__ M, int64_t rows,
+                                                   const double* __restrict__ Ginv, int RP,
+                                                   double* Y, double* YT, int64_t ldT, float* YF,
+                                                   int round32, const int* stop) {
+    if (stop && *stop) return;
+    extern __shared__ double msh[];  // 16 x (RP + 1)
+    const int64_t r0 = (int64_t)blockIdx.x * 16;
+    const int LD = RP + 1;
+    for (int e = threadIdx.x; e < 16 * RP; e += 256) {
+        const int rr = e / RP, qq = e - rr * RP;
+        msh[rr * LD + qq] = (r0 + rr < rows) ? (double)M[(r0 + rr) * RP + qq] : 0.0;
+    }
+    __syncthreads();
+    for (int kb = 0; kb < RP; kb += 256) {
+        const int k = kb + (int)threadIdx.x % (RP < 256 ? RP : 256);
+        const int rstep = RP < 256 ? 256 / RP : 1;
+        const int rl = RP < 256 ? (int)threadIdx.x / RP : 0;
+        if (k >= RP) continue;
+        for (int rr = rl; rr < 16; rr += rstep) {
+            const int64_t i = r0 + rr;
+            if (i >= rows) break;
+            double s0 = 0.0, s1 = 0.0;
+            for (int qq = 0; qq < RP; qq += 2) {
+                s0 = fma(msh[rr * LD + qq], Ginv[(int64_t)qq * RP + k], s0);
+                s1 = fma(msh[rr * LD + qq + 1], Ginv[(int64_t)(qq + 1) * RP + k], s1);
+            }
+            double s = s0 + s1;
+            if (round32) s = (double)(float)s;
+            Y[i * RP + k] = s;
+            if (YT) YT[(int64_t)k * ldT + i] = s;
+            if (YF) YF[i * RP + k] = (float)s;
+        }
+    }
+}
+
+void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, const double* Ginv,
+                      double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
+                      hipStream_t st) {
+    const size_t lds = (size_t)16 * (RP + 1) * sizeof(double);
+    const dim3 grid((unsigned)cdiv(rows, 16)), block(256);
+    if (Mf)
+        hipLaunchKernelGGL(k_apply_gen<float>, grid, block, lds, st, Mf, rows, Ginv, RP, Y, YT, ldT,
+                           YF, (int)round32, stop);
+    else
+        hipLaunchKernelGGL(k_apply_gen<double>, grid, block, lds, st, M, rows, Ginv, RP, Y, YT, ldT,
+                           YF, (int)round32, stop);
+    TRITD_CHECK_LAUNCH();
+}
+
+}  // namespace tritd

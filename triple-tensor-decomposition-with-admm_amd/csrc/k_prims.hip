@@ -132,6 +132,8 @@ void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* 
         TP_CASE(32)
         TP_CASE(48)
         TP_CASE(64)
+        TP_CASE(128)
+        TP_CASE(256)
         default:
             throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by triple_product");
     }

@@ -42,11 +42,14 @@ void launch_o_fixup(const Geom& g, const double* D, const double* YL, const doub
 // partial sums -> out[0..1] (fixed-order tree)
 void launch_reduce_pairs(const double* partial, int n, double* out, const int* stop, hipStream_t st);
 // both in one launch (single GPU: nothing to all-reduce in between)
+// single: D is of class single, so errHist(k) = single(norm/normD + norm/normD)
+// with the norms rounded to single (MATLAB class rules)
 void launch_reduce_finish(const double* partial, int n, double normD, int k, double tol,
-                          double* errHist, double* errL, double* errO, int* ctrl, hipStream_t st);
+                          double* errHist, double* errL, double* errO, int* ctrl, bool single,
+                          hipStream_t st);
 // errHist bookkeeping + stop test (triple_decomp_ADMM.m:59,63)
 void launch_finish(const double* ss, double normD, int k, double tol, double* errHist, double* errL,
-                   double* errO, int* ctrl, hipStream_t st);
+                   double* errO, int* ctrl, bool single, hipStream_t st);
 
 // ---- contractions and small linear algebra (k_contract.hip) ---------------
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
@@ -86,5 +89,58 @@ void launch_from_tm(const Geom& g, const double* src, double* dst, int64_t ld, h
 void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hipStream_t st);
 void launch_design(char which, const double* P, const double* Q, int64_t nP, int64_t nQ, int r,
                    double* out, hipStream_t st);
+
+// ---------------------------------------------------------------------------
+// fp32 data path (D of class single): T, O, E, Y_L, Y_O, W and
+// the mode contractions in fp32; factors, Grams and solves in fp64.
+// RP in {16, 32, 48, 64, 128, 256}.
+// ---------------------------------------------------------------------------
+struct IterScalars32 {
+    float muL, muO, invL, invO, thr, den, invL_next;  // MATLAB: double scalar -> single
+};
+struct K5Args32 {
+    const float* D;
+    float* O;
+    float* E;   // dense E: only tiles whose compact slot overflowed
+    float* CE;  // compact E: one 64-float slot per tile (k_admm32.hip)
+    float* YL;
+    float* YO;
+    float* T;
+    float* Wk;
+    const double* Ah;
+    const double* Bh;
+    const float* ChF;  // C^ (n3p x RP) in single (the values are single-rounded already)
+    double* partial;   // [grid][2] sums of resL^2, resO^2
+    int64_t n1p, n2, n3p, plane, tiles, ntt;
+    IterScalars32 s;
+    const int* stop;
+    unsigned long long* dense_tiles;
+};
+constexpr int CE32_SLOT = 64;  // floats per compact-E slot (8 mask words + 56 values)
+bool rp_supported32(int RP);
+int padded_rank32(int R);
+void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st);
+void launch_to_tm32(const Geom& g, const float* src, int64_t ld, float* dst, hipStream_t st);
+void launch_from_tm32(const Geom& g, const float* src, float* dst, int64_t ld, hipStream_t st);
+void launch_sumsq32(const Geom& g, const float* X, double* partial, int nblocks, hipStream_t st);
+void launch_o_fixup32(const Geom& g, const float* D, const float* YL, const float* T,
+                      float invL_next, float* O, hipStream_t st);
+void launch_ce_expand32(const Geom& g, const float* CE, float* E, hipStream_t st);
+void launch_pool_probe32(const Geom& g, float* D, float* YL, float* YO, float* T, float* CE,
+                         hipStream_t st);
+void launch_widen(const float* x, int64_t n, double* y, hipStream_t st);
+void launch_m1_32(const Geom& g, const float* Wk, const double* Bh, float* M1, const int* stop,
+                  hipStream_t st);
+void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
+                  hipStream_t st);
+int m3_parts32(const Geom& g);
+void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double* Bh, double* part,
+                  double* M3, const int* stop, hipStream_t st);
+// Y = M * Ginv for any RP; M double or single (Mf); round32: results rounded to
+// single (then stored as double; MATLAB's (X*F')*pinv(G) is single for single
+// data); YT transposed copy, YF single copy (either may be null)
+void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, const double* Ginv,
+                      double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
+                      hipStream_t st);
 
 }  // namespace tritd

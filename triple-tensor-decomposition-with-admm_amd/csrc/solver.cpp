@@ -70,7 +70,7 @@ void unpack_C(const Geom& g, const std::vector<double>& Ch, double* C) {
 }
 
 // ---------------------------------------------------------------------------
-Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n2, int64_t n3,
+Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2, int64_t n3,
                  int64_t i0, int64_t i1, int r, const tritd_opts& o, const double* A0,
                  const double* B0, const double* C0, tritd_comm* comm, uint32_t flags,
                  hipStream_t shared_stream, bool defer_normD)
@@ -83,6 +83,9 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         own_stream_ = true;
     }
     g_ = make_geom(n1, n2, n3, i0, i1, r);
+    f32_ = (flags & TRITD_SESSION_F32) != 0;
+    es_ = f32_ ? sizeof(float) : sizeof(double);
+    if (f32_) g_.RP = padded_rank32(g_.R);
     overlap_ = (comm == nullptr) && (shared_stream == nullptr);
     {
         const char* ov = std::getenv("TRITD_OVERLAP");
@@ -96,7 +99,9 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         for (hipEvent_t* e : {&evAtA_, &evBtB_, &evCtC_, &evSA_, &evSB_, &evSC_})
             TRITD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
-    if (!rp_supported(g_.RP)) throw Error(TRITD_ERR_UNSUPPORTED, "r must be in 1..8 for the fp64 path");
+    if (f32_ ? !rp_supported32(g_.RP) : !rp_supported(g_.RP))
+        throw Error(TRITD_ERR_UNSUPPORTED,
+                    f32_ ? "r must be in 1..16 for the fp32 path" : "r must be in 1..8 for the fp64 path");
 
     // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
     mu_.resize((size_t)o_.maxIter + 2);
@@ -116,29 +121,31 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
         // the same HBM channel
         const char* sg = std::getenv("TRITD_STAGGER");
         const size_t stagger = sg ? (size_t)std::atoll(sg) : 256;  // measured: tools/stagger_sweep.py
-        const size_t slot = round_up((int64_t)(Np * sizeof(double) + 5 * stagger), 4096);
+        const size_t slot = round_up((int64_t)(Np * es_ + 5 * stagger), 4096);
         const size_t pool_bytes = 6 * slot;
-        CE_.alloc((size_t)(g_.Ntm / 256) * CE_SLOT);  // before probing: the probe streams it
+        // compact E: 256 B per tile in either data type (before probing: the probe streams it)
+        CE_.alloc_bytes((size_t)(g_.Ntm / 256) * 256);
         pool_.p = probe_pool(pool_bytes, slot, stagger);
-        TRITD_HIP(hipMemsetAsync(CE_.p, 0, CE_.n * sizeof(double), st_));
+        TRITD_HIP(hipMemsetAsync(CE_.p, 0, CE_.bytes(), st_));
         pool_.n = pool_bytes / sizeof(double);
         int q = 0;
         for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
-            b->p = pool_.p + (q * slot + q * stagger) / sizeof(double);
-            b->n = Np;
+            b->p = reinterpret_cast<double*>(reinterpret_cast<char*>(pool_.p) + q * slot + q * stagger);
+            b->n = (Np * es_) / sizeof(double);
             b->owned = false;
-            TRITD_HIP(hipMemsetAsync(b->p, 0, Np * sizeof(double), st_));
+            TRITD_HIP(hipMemsetAsync(b->p, 0, Np * es_, st_));
             ++q;
         }
     }
-    Wk_.alloc((size_t)g_.RP * g_.plane);
-    TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.n * sizeof(double), st_));
+    Wk_.alloc_bytes((size_t)g_.RP * g_.plane * es_);
+    TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.bytes(), st_));
+    if (f32_) ChF_.alloc_bytes((size_t)g_.n3p * g_.RP * sizeof(float));
     Ah_.alloc(g_.n1p * g_.RP);
     AhT_.alloc((size_t)g_.RP * g_.n1p);
     Bh_.alloc(g_.n2 * g_.RP);
     Ch_.alloc(g_.n3p * g_.RP);
     ChT_.alloc((size_t)g_.RP * g_.n3p);
-    M1_.alloc(g_.n1p * g_.RP);
+    M1_.alloc_bytes((size_t)g_.n1p * g_.RP * es_);
     Ginv_.alloc((size_t)g_.RP * g_.RP);
     if (overlap_) {
         GinvA_.alloc((size_t)g_.RP * g_.RP);
@@ -151,7 +158,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     red2_.alloc(red2_count());
     red3_.alloc(2);
     k5part_.alloc(2 * (size_t)k5_grid(g_));
-    m3part_.alloc((size_t)m3_parts(g_) * g_.n3p * g_.RP);
+    m3part_.alloc((size_t)(f32_ ? m3_parts32(g_) : m3_parts(g_)) * g_.n3p * g_.RP);
     sqpart_.alloc(2 * (size_t)sumsq_blocks(g_));
     const size_t mi = o_.maxIter > 0 ? (size_t)o_.maxIter : 1;
     errHist_.alloc(mi);
@@ -164,15 +171,20 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
 
     // D -> tile-major device layout (one-off)
     if (g_.n1l > 0 && n2 * n3 > 0) {
+        auto to_tm = [&](const void* src, int64_t ld) {
+            if (f32_)
+                launch_to_tm32(g_, static_cast<const float*>(src), ld, D_.f(), st_);
+            else
+                launch_to_tm(g_, static_cast<const double*>(src), ld, D_.p, st_);
+        };
         if (flags & TRITD_SESSION_D_ON_DEVICE) {
-            launch_to_tm(g_, D, ldD, D_.p, st_);
+            to_tm(D, ldD);
         } else {
             DBuf tmp;
-            tmp.alloc((size_t)(g_.n1l * n2 * n3));
-            TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * sizeof(double), D, ldD * sizeof(double),
-                                       g_.n1l * sizeof(double), (size_t)(n2 * n3),
-                                       hipMemcpyHostToDevice, st_));
-            launch_to_tm(g_, tmp.p, g_.n1l, D_.p, st_);
+            tmp.alloc_bytes((size_t)(g_.n1l * n2 * n3) * es_);
+            TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * es_, D, ldD * es_, g_.n1l * es_,
+                                       (size_t)(n2 * n3), hipMemcpyHostToDevice, st_));
+            to_tm(tmp.p, g_.n1l);
             TRITD_HIP(hipStreamSynchronize(st_));
         }
     }
@@ -180,7 +192,10 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
 
     // normD = norm(D(:))  (:28)
     const int nb = sumsq_blocks(g_);
-    launch_sumsq_padded(g_, D_.p, sqpart_.p, nb, st_);
+    if (f32_)
+        launch_sumsq32(g_, D_.f(), sqpart_.p, nb, st_);
+    else
+        launch_sumsq_padded(g_, D_.p, sqpart_.p, nb, st_);
     launch_reduce_pairs(sqpart_.p, nb, red3_.p, nullptr, st_);
     if (!defer_normD) {
         allreduce(red3_.p, 2);
@@ -192,16 +207,7 @@ Session::Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n
     launch_gram(g_.RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
 
     // T of iteration 1 (:33) and W = T x3 C0 for update_A/update_B
-    K5Args a{};
-    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.CE = CE_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
-    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
-    a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
-    a.ntt = g_.ntt;
-    a.s = scalars(1);
-    a.stop = ctrl_;
-    a.dense_tiles = dense_tiles();
-    a.rot = rot_;
-    if (o_.maxIter > 0) launch_k5(g_, a, /*prologue=*/true, st_);
+    if (o_.maxIter > 0) launch_k5_any(1, /*prologue=*/true);
     if (overlap_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
         TRITD_HIP(hipEventRecord(evCtC_, st_));
         TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
@@ -231,6 +237,7 @@ void Session::set_normD_from_red3() {
     TRITD_HIP(hipMemcpyAsync(ss, red3_.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st_));
     TRITD_HIP(hipStreamSynchronize(st_));
     normD_ = std::sqrt(ss[0]);
+    if (f32_) normD_ = (double)(float)normD_;  // norm of a single array is single
 }
 
 void Session::upload_factors(const double* A0, const double* B0, const double* C0) {
@@ -243,6 +250,11 @@ void Session::upload_factors(const double* A0, const double* B0, const double* C
     TRITD_HIP(hipMemcpy(Bh_.p, Bh.data(), Bh.size() * sizeof(double), hipMemcpyHostToDevice));
     TRITD_HIP(hipMemcpy(Ch_.p, Ch.data(), Ch.size() * sizeof(double), hipMemcpyHostToDevice));
     TRITD_HIP(hipMemcpy(ChT_.p, ChT.data(), ChT.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (f32_) {
+        std::vector<float> cf(Ch.size());
+        for (size_t e = 0; e < Ch.size(); ++e) cf[e] = (float)Ch[e];
+        TRITD_HIP(hipMemcpy(ChF_.p, cf.data(), cf.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
 }
 
 IterScalars Session::scalars(int k) const {
@@ -255,6 +267,93 @@ IterScalars Session::scalars(int k) const {
     s.den = s.muL + s.muO;
     s.invL_next = 1.0 / mu_[(size_t)k];
     return s;
+}
+
+IterScalars32 Session::scalars32(int k) const {
+    // MATLAB: a double scalar meeting a single array is converted to single
+    const IterScalars d = scalars(k);
+    IterScalars32 s;
+    s.muL = (float)d.muL;
+    s.muO = (float)d.muO;
+    s.invL = (float)d.invL;
+    s.invO = (float)d.invO;
+    s.thr = (float)d.thr;
+    s.den = (float)d.den;
+    s.invL_next = (float)d.invL_next;
+    return s;
+}
+
+void Session::do_m1() {
+    if (f32_)
+        launch_m1_32(g_, Wk_.f(), Bh_.p, M1_.f(), ctrl_, st_);
+    else
+        launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+}
+
+void Session::do_m2(double* M2) {
+    if (f32_)
+        launch_m2_32(g_, Wk_.f(), AhT_.p, M2, ctrl_, st_);
+    else
+        launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
+}
+
+void Session::do_m3() {
+    if (f32_)
+        launch_m3_32(g_, T_.f(), Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+    else
+        launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+}
+
+// (X*F')*pinv(G): fp64 path through the LDS-staged apply (RP <= 64); fp32
+// path single in, single-rounded out (MATLAB single * double = single)
+void Session::do_apply_A(const double* Ginv) {
+    if (f32_)
+        launch_apply_gen(g_.RP, nullptr, M1_.f(), g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
+                         true, ctrl_, st_);
+    else
+        launch_apply(g_.RP, M1_.p, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+}
+
+void Session::do_apply_B(const double* M2, const double* Ginv) {
+    if (f32_)
+        launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, true, ctrl_,
+                         st_);
+    else
+        launch_apply(g_.RP, M2, g_.n2, Ginv, Bh_.p, nullptr, 0, ctrl_, st_);
+}
+
+void Session::do_apply_C(const double* Ginv) {
+    if (f32_)
+        launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ChF_.f(),
+                         true, ctrl_, st_);
+    else
+        launch_apply(g_.RP, red2_.p, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+}
+
+void Session::launch_k5_any(int k, bool prologue) {
+    if (f32_) {
+        K5Args32 a{};
+        a.D = D_.f(); a.O = O_.f(); a.E = E_.f(); a.CE = CE_.f(); a.YL = YL_.f(); a.YO = YO_.f();
+        a.T = T_.f(); a.Wk = Wk_.f();
+        a.Ah = Ah_.p; a.Bh = Bh_.p; a.ChF = ChF_.f(); a.partial = k5part_.p;
+        a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
+        a.ntt = g_.ntt;
+        a.s = scalars32(k);
+        a.stop = ctrl_;
+        a.dense_tiles = dense_tiles();
+        launch_k5_32(g_, a, prologue, st_);
+        return;
+    }
+    K5Args a{};
+    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.CE = CE_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
+    a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
+    a.ntt = g_.ntt;
+    a.s = scalars(k);
+    a.stop = ctrl_;
+    a.dense_tiles = dense_tiles();
+    a.rot = rot_;
+    launch_k5(g_, a, prologue, st_);
 }
 
 void Session::allreduce(double* buf, int64_t count) {
@@ -274,11 +373,11 @@ void Session::phaseA(int k) {
     const int RP = g_.RP;
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
-    launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    do_m1();
     launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, Ginv_.p, ctrl_ + 2, ctrl_, st_);
-    launch_apply(RP, M1_.p, g_.n1p, Ginv_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    do_apply_A(Ginv_.p);
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
-    launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
+    do_m2(M2);
 }
 
 void Session::phaseB(int k) {
@@ -287,10 +386,10 @@ void Session::phaseB(int k) {
     const double* M2 = red1_.p;
     const double* AtA = red1_.p + g_.n2 * RP;
     launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, Ginv_.p, ctrl_ + 2, ctrl_, st_);
-    launch_apply(RP, M2, g_.n2, Ginv_.p, Bh_.p, nullptr, 0, ctrl_, st_);
+    do_apply_B(M2, Ginv_.p);
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
-    launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+    do_m3();
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
 }
 
@@ -298,7 +397,7 @@ void Session::phaseC(int k) {
     const int RP = g_.RP;
     const double* AtA = red1_.p + g_.n2 * RP;
     launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :93 ridge
-    launch_apply(RP, red2_.p, g_.n3p, Ginv_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+    do_apply_C(Ginv_.p);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     launch_k5_full(k, /*fused_finish=*/false);
 }
@@ -337,14 +436,22 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
         TRITD_HIP(hipEventCreate(&e0));
         TRITD_HIP(hipEventCreate(&e1));
         for (size_t c = 0; c < cand.size(); ++c) {
-            double* f[6];
-            for (int q = 0; q < 6; ++q) f[q] = cand[c] + (q * slot + q * stagger) / sizeof(double);
+            char* f[6];
+            for (int q = 0; q < 6; ++q) f[q] = reinterpret_cast<char*>(cand[c]) + q * slot + q * stagger;
             // pool order: D, O, E, YL, YO, T
-            launch_pool_probe(g_, f[0], f[3], f[4], f[5], CE_.p, st_);  // warm
+            auto probe = [&] {
+                if (f32_)
+                    launch_pool_probe32(g_, (float*)f[0], (float*)f[3], (float*)f[4], (float*)f[5],
+                                        CE_.f(), st_);
+                else
+                    launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[4],
+                                      (double*)f[5], CE_.p, st_);
+            };
+            probe();  // warm
             float ms = 1e30f;
             for (int r = 0; r < 2; ++r) {
                 TRITD_HIP(hipEventRecord(e0, st_));
-                launch_pool_probe(g_, f[0], f[3], f[4], f[5], CE_.p, st_);
+                probe();
                 TRITD_HIP(hipEventRecord(e1, st_));
                 TRITD_HIP(hipEventSynchronize(e1));
                 float x = 0.f;
@@ -364,21 +471,12 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
 }
 
 void Session::launch_k5_full(int k, bool fused_finish) {
-    K5Args a{};
-    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.CE = CE_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
-    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
-    a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
-    a.ntt = g_.ntt;
-    a.s = scalars(k);
-    a.stop = ctrl_;
-    a.dense_tiles = dense_tiles();
-    a.rot = rot_;
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
-    launch_k5(g_, a, /*prologue=*/false, st_);
+    launch_k5_any(k, /*prologue=*/false);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 2], st_));
     if (fused_finish)  // single GPU: no all-reduce between the norm sums and the stop test
         launch_reduce_finish(k5part_.p, k5_grid(g_), normD_, k, o_.tol, errHist_.p, errL_.p,
-                             errO_.p, ctrl_, st_);
+                             errO_.p, ctrl_, f32_, st_);
     else
         launch_reduce_pairs(k5part_.p, k5_grid(g_), red3_.p, ctrl_, st_);
 }
@@ -396,18 +494,18 @@ void Session::iterate_overlapped(int k) {
     // main: M1 -> apply A -> M2 -> apply B -> K2 -> apply C -> K5 -> norms/finish
     // side: Gram A -> solve B | Gram B -> solve C | Gram C -> solve A(k+1)
     hipStream_t gs = (ovmode_ >= 3) ? side_ : st_;
-    launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    do_m1();
     TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
-    launch_apply(RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    do_apply_A(GinvA_.p);
     if (gs == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evAtA_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
     if (gs == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
     launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, GinvB_.p, ctrl_ + 2, ctrl_, side_);
     TRITD_HIP(hipEventRecord(evSB_, side_));
-    launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
+    do_m2(M2);
     TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
-    launch_apply(RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, ctrl_, st_);
+    do_apply_B(M2, GinvB_.p);
     if (gs == st_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
@@ -415,10 +513,10 @@ void Session::iterate_overlapped(int k) {
     launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
-    launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+    do_m3();
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
-    launch_apply(RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+    do_apply_C(GinvC_.p);
     if (gs == st_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
@@ -429,7 +527,7 @@ void Session::iterate_overlapped(int k) {
 }
 
 void Session::phaseD(int k) {
-    launch_finish(red3_.p, normD_, k, o_.tol, errHist_.p, errL_.p, errO_.p, ctrl_, st_);
+    launch_finish(red3_.p, normD_, k, o_.tol, errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_);
 }
 
 void Session::maybe_print(int k) {
@@ -518,7 +616,7 @@ void Session::kernel_ms(double* k5, double* m3, double* it, int* samples) {
     if (samples) *samples = acc_n_;
 }
 
-void Session::get(double* A, double* B, double* C, double* O, double* E, int64_t ldOE,
+void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldOE,
                   double* errHist, int* iters) {
     int done = 0, stopped = 0;
     sync(&done, &stopped);
@@ -537,18 +635,30 @@ void Session::get(double* A, double* B, double* C, double* O, double* E, int64_t
         TRITD_HIP(hipMemcpy(h.data(), Ch_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
         unpack_C(g_, h, C);
     }
-    if (O && g_.n1l > 0 && done > 0)  // O of iteration `done` from D, Y_L, T (K5 does not store it)
-        launch_o_fixup(g_, D_.p, YL_.p, T_.p, 1.0 / mu_[(size_t)done], O_.p, st_);
-    if (E && g_.n1l > 0) launch_ce_expand(g_, CE_.p, E_.p, st_);  // E lives in compact form
+    if (O && g_.n1l > 0 && done > 0) {  // O of iteration `done` from D, Y_L, T (K5 does not store it)
+        if (f32_)
+            launch_o_fixup32(g_, D_.f(), YL_.f(), T_.f(), (float)(1.0 / mu_[(size_t)done]), O_.f(),
+                             st_);
+        else
+            launch_o_fixup(g_, D_.p, YL_.p, T_.p, 1.0 / mu_[(size_t)done], O_.p, st_);
+    }
+    if (E && g_.n1l > 0) {  // E lives in compact form
+        if (f32_)
+            launch_ce_expand32(g_, CE_.f(), E_.f(), st_);
+        else
+            launch_ce_expand(g_, CE_.p, E_.p, st_);
+    }
     if ((O || E) && g_.n1l > 0) {
         DBuf tmp;
-        tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));
+        tmp.alloc_bytes((size_t)(g_.n1l * g_.n2 * g_.n3) * es_);
         for (auto pr : {std::make_pair(O, &O_), std::make_pair(E, &E_)}) {
             if (!pr.first) continue;
-            launch_from_tm(g_, pr.second->p, tmp.p, g_.n1l, st_);
-            TRITD_HIP(hipMemcpy2DAsync(pr.first, ldOE * sizeof(double), tmp.p, g_.n1l * sizeof(double),
-                                       g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
-                                       hipMemcpyDeviceToHost, st_));
+            if (f32_)
+                launch_from_tm32(g_, pr.second->f(), tmp.f(), g_.n1l, st_);
+            else
+                launch_from_tm(g_, pr.second->p, tmp.p, g_.n1l, st_);
+            TRITD_HIP(hipMemcpy2DAsync(pr.first, ldOE * es_, tmp.p, g_.n1l * es_, g_.n1l * es_,
+                                       (size_t)(g_.n2 * g_.n3), hipMemcpyDeviceToHost, st_));
             TRITD_HIP(hipStreamSynchronize(st_));
         }
     }
@@ -566,12 +676,19 @@ void Session::counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch) {
     if (tiles_per_launch) *tiles_per_launch = g_.Ntm / 256;
 }
 
-void Session::rre_parts(const double* dX, int64_t ldX, double* num, double* den) {
+void Session::rre_parts(const void* dX, int64_t ldX, double* num, double* den) {
     TRITD_HIP(hipSetDevice(device_));
-    DBuf Xp, part, out;
+    DBuf Xp, Xd, part, out;
     Xp.alloc((size_t)g_.Np);
     TRITD_HIP(hipMemsetAsync(Xp.p, 0, Xp.n * sizeof(double), st_));
-    TRITD_HIP(hipMemcpy2DAsync(Xp.p, g_.n1p * sizeof(double), dX, ldX * sizeof(double),
+    const double* src = static_cast<const double*>(dX);
+    if (f32_) {  // the reference tensor in single: widen (exactly) to double
+        const int64_t cnt = (g_.n2 * g_.n3 - 1) * ldX + g_.n1l;
+        Xd.alloc((size_t)cnt);
+        launch_widen(static_cast<const float*>(dX), cnt, Xd.p, st_);
+        src = Xd.p;
+    }
+    TRITD_HIP(hipMemcpy2DAsync(Xp.p, g_.n1p * sizeof(double), src, ldX * sizeof(double),
                                g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
                                hipMemcpyDeviceToDevice, st_));
     const int grid = tp_grid(g_);

@@ -29,6 +29,9 @@ struct DBuf {
         n = count;
         TRITD_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(double)));
     }
+    void alloc_bytes(size_t bytes) { alloc((bytes + sizeof(double) - 1) / sizeof(double)); }
+    float* f() const { return reinterpret_cast<float*>(p); }
+    size_t bytes() const { return n * sizeof(double); }
 };
 
 // Host-side layout conversions between the reference shapes and the device
@@ -42,7 +45,8 @@ void unpack_C(const Geom& g, const std::vector<double>& Ch, double* C);
 
 class Session {
    public:
-    Session(int device, const double* D, int64_t ldD, int64_t n1, int64_t n2, int64_t n3, int64_t i0,
+    // D: double, or float when flags has TRITD_SESSION_F32 (the fp32 data path)
+    Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2, int64_t n3, int64_t i0,
             int64_t i1, int r, const tritd_opts& o, const double* A0, const double* B0,
             const double* C0, tritd_comm* comm, uint32_t flags, hipStream_t shared_stream = nullptr,
             bool defer_normD = false);
@@ -51,9 +55,12 @@ class Session {
     // Enqueue iterations (full collective schedule; used without a virtual group)
     void run(int iters);
     void sync(int* done, int* stopped);
-    void get(double* A, double* B, double* C, double* O, double* E, int64_t ldOE, double* errHist,
+    // O, E: double, or float for an fp32 session
+    void get(double* A, double* B, double* C, void* O, void* E, int64_t ldOE, double* errHist,
              int* iters);
-    void rre_parts(const double* dX, int64_t ldX, double* num, double* den);
+    // dX: device tensor of the session's data type
+    void rre_parts(const void* dX, int64_t ldX, double* num, double* den);
+    bool is_f32() const { return f32_; }
     void counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch);
     void set_timing(bool on);
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
@@ -97,6 +104,18 @@ class Session {
     int probe_pick_ = 0;
     void upload_factors(const double* A0, const double* B0, const double* C0);
     IterScalars scalars(int k) const;
+    IterScalars32 scalars32(int k) const;
+    // data-type dispatch of the per-iteration kernels
+    void do_m1();
+    void do_m2(double* M2);
+    void do_m3();
+    void do_apply_A(const double* Ginv);
+    void do_apply_B(const double* M2, const double* Ginv);
+    void do_apply_C(const double* Ginv);
+    void launch_k5_any(int k, bool prologue);
+    bool f32_ = false;
+    size_t es_ = sizeof(double);  // bytes per element of D, O, E, Y_L, Y_O, T, W, M1
+    DBuf ChF_;                    // C^ in single (fp32 path)
 
     int device_;
     hipStream_t st_ = nullptr;

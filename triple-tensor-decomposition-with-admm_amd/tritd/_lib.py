@@ -22,6 +22,7 @@ OPT_MU, OPT_RHO, OPT_LAMBDA, OPT_LAMBDA2, OPT_MAXITER, OPT_TOL, OPT_DISP = (1 <<
 OPT_BITS = {"mu": OPT_MU, "rho": OPT_RHO, "lambda": OPT_LAMBDA, "lambda2": OPT_LAMBDA2,
             "maxIter": OPT_MAXITER, "tol": OPT_TOL, "disp": OPT_DISP}
 SESSION_D_ON_DEVICE = 1
+SESSION_F32 = 2
 
 
 class TritdError(RuntimeError):
@@ -51,12 +52,16 @@ SIGNATURES = {
     "tritd_device_count": (C.c_int, [C.POINTER(i32)]),
     "tritd_admm_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp, vp, vp, vp,
                                  vp, vp, vp, C.POINTER(i32), i32]),
+    "tritd_admm_f32": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp, vp, vp, vp,
+                                 vp, vp, vp, C.POINTER(i32), i32]),
     "tritd_session_create": (C.c_int, [C.POINTER(vp), i32, vp, i64, i64, i64, i64, i64, i64, i32,
                                        C.POINTER(Opts), vp, vp, vp, vp, C.c_uint32]),
     "tritd_session_run": (C.c_int, [vp, i32]),
     "tritd_session_sync": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32)]),
     "tritd_session_get": (C.c_int, [vp, vp, vp, vp, vp, vp, i64, vp, C.POINTER(i32)]),
     "tritd_session_rre_parts": (C.c_int, [vp, vp, i64, dp, dp]),
+    "tritd_session_get_f32": (C.c_int, [vp, vp, vp, vp, vp, vp, i64, vp, C.POINTER(i32)]),
+    "tritd_session_rre_parts_f32": (C.c_int, [vp, vp, i64, dp, dp]),
     "tritd_session_set_timing": (C.c_int, [vp, i32]),
     "tritd_session_kernel_ms": (C.c_int, [vp, dp, dp, dp, C.POINTER(i32)]),
     "tritd_session_probe": (C.c_int, [vp, dp, i32, C.POINTER(i32), C.POINTER(i32)]),

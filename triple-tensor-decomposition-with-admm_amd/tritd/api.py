@@ -100,8 +100,11 @@ def triple_decomp_ADMM(D, r, opts, A0=None, B0=None, C0=None, *, device=-1, retu
     Extra outputs beyond the reference signature: E (``return_E``) and the
     iteration count (``return_iters``).  ``virtual_shards=P`` runs the mode-1
     sharded schedule as P shards on one device (rehearsal of the multi-GPU
-    path)."""
+    path).  A float32 D runs the single-class path (MATLAB semantics of a
+    `single` D: O, E float32; A, B, C, errHist float64), r <= 16."""
     o = make_opts(opts)
+    if np.asarray(D).dtype == np.float32:
+        return _admm_f32(D, r, o, opts, A0, B0, C0, device, return_E, return_iters)
     D = _fortran(D)
     n1, n2, n3 = _size3(D)
     r = int(r)
@@ -127,6 +130,32 @@ def triple_decomp_ADMM(D, r, opts, A0=None, B0=None, C0=None, *, device=-1, retu
                                  C.byref(k), int(device)))
     errHist = errHist[: k.value].copy()  # :68 errHist = errHist(1:k)
     out = [A, B, Cf, O, errHist]
+    if return_E:
+        out.append(E)
+    if return_iters:
+        out.append(k.value)
+    return tuple(out)
+
+
+def _admm_f32(D, r, o, opts, A0, B0, C0, device, return_E, return_iters):
+    D = np.asfortranarray(D, dtype=np.float32)
+    n1, n2, n3 = _size3(D)
+    r = int(r)
+    if A0 is None or B0 is None or C0 is None:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, opts)
+    else:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, dict(A0=A0, B0=B0, C0=C0))
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cf = np.zeros((r, r, n3), order="F")
+    O = np.zeros((n1, n2, n3), order="F", dtype=np.float32)
+    E = np.zeros((n1, n2, n3), order="F", dtype=np.float32)
+    errHist = np.zeros(max(o.maxIter, 1))
+    k = _lib.i32(0)
+    check(lib.tritd_admm_f32(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+                             _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), _ptr(errHist),
+                             C.byref(k), int(device)))
+    out = [A, B, Cf, O, errHist[: k.value].copy()]
     if return_E:
         out.append(E)
     if return_iters:
@@ -206,23 +235,27 @@ class Session:
     """One mode-1 shard [i0, i1) of an n1 x n2 x n3 problem on one GPU.
 
     D is either a host numpy array holding the shard (column-major, leading
-    dimension ldD) or, with ``d_device_ptr``, a device pointer."""
+    dimension ldD) or, with ``d_device_ptr``, a device pointer.  ``dtype``
+    float32 (or a float32 D) selects the single-class path."""
 
     def __init__(self, r, opts, A0, B0, C0, *, n1, n2, n3, i0=0, i1=None, D=None,
-                 d_device_ptr=None, ldD=None, device=0, comm=None):
+                 d_device_ptr=None, ldD=None, device=0, comm=None, dtype=None):
         self._s = C.c_void_p()
         o = make_opts(opts)
         i1 = n1 if i1 is None else i1
         A0 = _fortran(A0)
         B0 = _fortran(B0)
         C0 = _fortran(C0)
-        flags = 0
+        if dtype is None:
+            dtype = np.asarray(D).dtype if D is not None else np.float64
+        self.f32 = np.dtype(dtype) == np.float32
+        flags = _lib.SESSION_F32 if self.f32 else 0
         if d_device_ptr is not None:
             dptr = C.c_void_p(int(d_device_ptr))
             flags |= _lib.SESSION_D_ON_DEVICE
             ldD = ldD if ldD is not None else (i1 - i0)
         else:
-            D = _fortran(D)
+            D = np.asfortranarray(D, dtype=np.float32 if self.f32 else np.float64)
             dptr = _ptr(D)
             ldD = ldD if ldD is not None else D.shape[0]
         self.n1, self.n2, self.n3, self.i0, self.i1, self.r = n1, n2, n3, i0, i1, r
@@ -245,18 +278,19 @@ class Session:
         A = np.zeros((n1, r, r), order="F")
         B = np.zeros((r, n2, r), order="F")
         Cf = np.zeros((r, r, n3), order="F")
-        O = np.zeros((nl, n2, n3), order="F")
-        E = np.zeros((nl, n2, n3), order="F")
+        dt = np.float32 if self.f32 else np.float64
+        O = np.zeros((nl, n2, n3), order="F", dtype=dt)
+        E = np.zeros((nl, n2, n3), order="F", dtype=dt)
         eh = np.zeros(max(self.maxIter, 1))
         k = _lib.i32(0)
-        check(lib.tritd_session_get(self._s, _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), nl,
-                                    _ptr(eh), C.byref(k)))
+        fn = lib.tritd_session_get_f32 if self.f32 else lib.tritd_session_get
+        check(fn(self._s, _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), nl, _ptr(eh), C.byref(k)))
         return dict(A=A, B=B, C=Cf, O=O, E=E, errHist=eh[: k.value].copy(), k=k.value)
 
     def rre_parts(self, dX_ptr, ldX):
         num, den = C.c_double(0), C.c_double(0)
-        check(lib.tritd_session_rre_parts(self._s, C.c_void_p(int(dX_ptr)), int(ldX),
-                                          C.byref(num), C.byref(den)))
+        fn = lib.tritd_session_rre_parts_f32 if self.f32 else lib.tritd_session_rre_parts
+        check(fn(self._s, C.c_void_p(int(dX_ptr)), int(ldX), C.byref(num), C.byref(den)))
         return num.value, den.value
 
     def probe(self):
