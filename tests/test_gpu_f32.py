@@ -70,6 +70,17 @@ def test_f32_vs_c_oracle(tritd, cref, shape, r, iters):
     _compare(tritd, cref, d["D"].astype(np.float32), r, opts, d["A0"], d["B0"], d["C0"])
 
 
+@pytest.mark.parametrize("shape,r,iters", [((96, 80, 72), 10, 12), ((80, 72, 64), 12, 10),
+                                           ((64, 64, 48), 16, 10)])
+def test_f32_large_rank_vs_c_oracle(tritd, cref, shape, r, iters):
+    """r = 9..16 (padded rank 128 / 256, config 5's r = 16): the blocked R x R
+    sweep (k_contract.hip k_solve_big) and the RP-general fp32 kernels."""
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(*shape, r, seed=2, init_seed=7)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=iters)
+    _compare(tritd, cref, d["D"].astype(np.float32), r, opts, d["A0"], d["B0"], d["C0"])
+
+
 @pytest.mark.parametrize("case", ["mixed_tiles", "all_dense"])
 def test_f32_compact_e_overflow_tiles(tritd, cref, case):
     """Compact E in fp32: 64-word slots, more than 56 nonzeros of a 256-element

@@ -4,15 +4,16 @@
 #include <cstdio>
 #include <vector>
 #include <cmath>
-int main() {
-    const int RP = 64, R = 64;
+#include <cstdlib>
+int main(int argc, char** argv) {
+    const int RP = argc > 1 ? atoi(argv[1]) : 64, R = argc > 2 ? atoi(argv[2]) : RP;
     std::vector<double> P(RP * RP), Q(RP * RP);
     // SPD Grams: X^T X of random 200 x 64
-    std::vector<double> X(200 * RP);
+    std::vector<double> X(400 * RP);
     unsigned s = 1;
     for (auto& x : X) { s = s * 1103515245u + 12345u; x = ((s >> 8) & 0xffff) / 65536.0 - 0.5; }
     for (int i = 0; i < RP; ++i) for (int j = 0; j < RP; ++j) {
-        double a = 0; for (int r = 0; r < 200; ++r) a += X[r * RP + i] * X[r * RP + j];
+        double a = 0; for (int r = 0; r < 400; ++r) a += X[r * RP + i] * X[r * RP + j];
         P[i * RP + j] = a; Q[i * RP + j] = 1.0 + 0.01 * ((i * 7 + j * 7) % 5);  // symmetric
     }
     double *dP, *dQ, *dG; int *flags, *stop;
@@ -34,6 +35,8 @@ int main() {
         double a = 0; for (int k = 0; k < R; ++k) a += G[i * RP + k] * (P[k * RP + j] * Q[k * RP + j] + (k == j ? 1e-3 : 0));
         err = fmax(err, fabs(a - (i == j)));
     }
-    printf("%s: %.2f us/solve  max|inv*G-I| %.2e\n", VARIANT, ms * 1000 / 200, err);
+    int fl = 0;
+    hipMemcpy(&fl, flags, 4, hipMemcpyDeviceToHost);
+    printf("%s RP=%d R=%d: %.2f us/solve  max|inv*G-I| %.2e  flag %d\n", VARIANT, RP, R, ms * 1000 / 200, err, fl);
     return 0;
 }

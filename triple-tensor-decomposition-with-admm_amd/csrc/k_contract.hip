@@ -420,6 +420,157 @@ __global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Ginv = inv(P o Q + alpha I) for RP in {128, 256} (fp32 path, r = 9..16):
+// blocked symmetric sweep, one 1024-thread workgroup.  The RP x RP matrix S
+// lives in Ginv (global, L2-resident); thread t owns column c = t % RP and
+// the ROWS = RP*RP/1024 rows of strip t / RP, and only ever touches its own
+// entries there (no cross-thread global traffic, so no L1 coherence
+// question); rows are shared through LDS.  Per block K of 16 pivots:
+//   panel <- S_K (rows K, all columns)                         (LDS)
+//   M = inv(S_KK): one wave sweeps the 16 x 16 block in registers (its
+//       pivots are the sequential sweep's pivots -> pinv-tolerance check)
+//   X = M S_K                                                  (LDS)
+//   S_ij -= sum_k S_ik X_kj (i, j outside K); S_Kj = X_Kj; S_iK = X_Ki;
+//   S_KK = -M            (= sweeping the 16 pivots one by one, blocked)
+// After all blocks S = -inv: Ginv = -S, identity pad zeroed.
+// ---------------------------------------------------------------------------
+constexpr int SB = 16;  // pivots per block (a 32-wide register sweep does not fit the 128 VGPRs of a 1024-thread block)
+
+template <int P>
+__device__ __forceinline__ void sweep32_step(double (&a)[SB], double* rowp, double* pv, int c) {
+    rowp[c] = a[P];  // lanes of equal c write equal values
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const double piv = rowp[P];
+    pv[P] = piv;
+    const double d = 1.0 / piv;
+    const bool pc = (c == P);
+    const double s = rowp[c] * d;
+    const double m = pc ? 0.0 : 1.0;
+    const double t = pc ? -d : s;
+#pragma unroll
+    for (int i = 0; i < SB; ++i) a[i] = m * a[i] - rowp[i] * t;
+    a[P] = t;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int... Ps>
+__device__ __forceinline__ void sweep32_all(double (&a)[SB], double* rowp, double* pv, int c,
+                                            std::integer_sequence<int, Ps...>) {
+    (sweep32_step<Ps>(a, rowp, pv, c), ...);
+}
+
+template <int RP>
+__global__ __launch_bounds__(1024) void k_solve_big(const double* __restrict__ P,
+                                                    const double* __restrict__ Q, int R,
+                                                    double alpha, double* S, int* flags,
+                                                    const int* stop) {
+    if (*stop) return;
+    constexpr int ROWS = RP * RP / 1024;
+    extern __shared__ double sh[];
+    double* panel = sh;              // [SB][RP]
+    double* X = panel + SB * RP;     // [SB][RP]
+    double* M = X + SB * RP;         // [SB][SB]
+    double* rowp = M + SB * SB;      // [64]
+    double* pivs = rowp + 64;        // [RP]
+    const int tid = threadIdx.x;
+    const int c = tid % RP, rb = tid / RP;
+    const int r0 = rb * ROWS;
+    // S = P o Q + alpha I in the leading R x R block, identity pad
+#pragma unroll 1
+    for (int q = 0; q < ROWS; ++q) {
+        const int i = r0 + q;
+        double v;
+        if (i < R && c < R) {
+            v = P[i * RP + c] * Q[i * RP + c];
+            if (i == c) v = v + alpha;
+        } else {
+            v = (i == c) ? 1.0 : 0.0;
+        }
+        S[i * RP + c] = v;
+    }
+    for (int k0 = 0; k0 < RP; k0 += SB) {
+        // panel <- rows K (each owner writes its own entries)
+    #pragma unroll 1
+    for (int q = 0; q < ROWS; ++q) {
+            const int i = r0 + q;
+            if (i >= k0 && i < k0 + SB) panel[(i - k0) * RP + c] = S[i * RP + c];
+        }
+        __syncthreads();
+        // M = inv(S_KK) by a register sweep of the 16 x 16 block in wave 0
+        // (a wave-uniform test: under a divergent one the sweep spills; the 4
+        // lane groups of the wave sweep identical copies)
+        if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
+            const int cc = tid & (SB - 1);
+            double a[SB];
+#pragma unroll
+            for (int i = 0; i < SB; ++i) a[i] = panel[i * RP + k0 + cc];
+            sweep32_all(a, rowp, pivs + k0, cc, std::make_integer_sequence<int, SB>{});
+#pragma unroll
+            for (int i = 0; i < SB; ++i) M[i * SB + cc] = -a[i];
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int e = tid; e < SB * RP; e += 1024) {  // X = M S_K
+            const int k = e / RP, jj = e - k * RP;
+            double x = 0.0;
+#pragma unroll 8
+            for (int l = 0; l < SB; ++l) x = fma(M[k * SB + l], panel[l * RP + jj], x);
+            X[e] = x;
+        }
+        __syncthreads();
+        const bool cK = c >= k0 && c < k0 + SB;
+        double xc[SB];  // this thread's column of X, reused by all its rows
+#pragma unroll
+        for (int k = 0; k < SB; ++k) xc[k] = X[k * RP + c];
+        // rows in chunks of 8: their L2 loads are in flight together
+#pragma unroll 1
+        for (int q0 = 0; q0 < ROWS; q0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = S[(r0 + q0 + u) * RP + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = r0 + q0 + u;
+                const bool iK = i >= k0 && i < k0 + SB;
+                double w = v[u];
+#pragma unroll
+                for (int k = 0; k < SB; ++k) w = w - panel[k * RP + i] * xc[k];
+                if (iK && cK)
+                    w = -M[(i - k0) * SB + (c - k0)];
+                else if (iK)
+                    w = X[(i - k0) * RP + c];
+                else if (cK)
+                    w = X[(c - k0) * RP + i];
+                S[i * RP + c] = w;
+            }
+        }
+        __syncthreads();
+    }
+    // Ginv = -S, pad zeroed (each thread its own entries)
+#pragma unroll 1
+    for (int q = 0; q < ROWS; ++q) {
+        const int i = r0 + q;
+        S[i * RP + c] = (i < R && c < R) ? -S[i * RP + c] : 0.0;
+    }
+    if (tid == 0) {
+        double minpiv = 1e308, maxpiv = 0.0;
+        for (int p = 0; p < R; ++p) {
+            minpiv = fmin(minpiv, pivs[p]);
+            maxpiv = fmax(maxpiv, pivs[p]);
+        }
+        const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);
+        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
+    }
+}
+
+static size_t solve_big_lds(int RP) {
+    return (size_t)(2 * SB * RP + SB * SB + 64 + RP) * sizeof(double);
+}
+
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
                   int* flags, const int* stop, hipStream_t st) {
 #define SOLVE_CASE(RPV)                                                                      \
@@ -432,8 +583,21 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
         SOLVE_CASE(32)
         SOLVE_CASE(48)
         SOLVE_CASE(64)
+        case 128:
+        case 256: {
+            const size_t lds = solve_big_lds(RP);
+            auto kern = RP == 128 ? k_solve_big<128> : k_solve_big<256>;
+            static bool attr[2] = {false, false};
+            if (!attr[RP == 256]) {
+                TRITD_HIP(hipFuncSetAttribute((const void*)kern,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                attr[RP == 256] = true;
+            }
+            hipLaunchKernelGGL(kern, dim3(1), dim3(1024), lds, st, P, Q, R, alpha, Ginv, flags, stop);
+            break;
+        }
         default:
-            throw Error(TRITD_ERR_UNSUPPORTED, "R > 64 solve");
+            throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
     }
 #undef SOLVE_CASE
     TRITD_CHECK_LAUNCH();
