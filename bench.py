@@ -1,7 +1,9 @@
 """TriTD-ADMM benchmark: ADMM iterations/s + final RRE on the synthetic
-512x512x512 r=8 fp64 workload (BASELINE.json configs[3]).
+512x512x512 r=8 fp64 workload (BASELINE.json configs[3] = SURVEY.md §8d
+config 4, the default) or the 2048x2048x256 r=16 fp32 workload
+(configs[4] = config 5, ``--config 5``).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A "step" is one ADMM iteration (triple_decomp_ADMM.m:31-66) over the whole
@@ -25,8 +27,9 @@ sys.path.insert(0, PKG)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-N_DEFAULT = 512
-R_DEFAULT = 8
+F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA, dense
+# SURVEY.md §8d workloads: (n1, n2, n3, r, dtype)
+CONFIGS = {4: (512, 512, 512, 8, "f64"), 5: (2048, 2048, 256, 16, "f32")}
 
 
 def ensure_built():
@@ -49,22 +52,25 @@ def cpu_baseline(D, r, opts, A0, B0, C0, iters):
         out = tritd_ref.admm(lib, D, r, opts, A0, B0, C0, max_iters=iters)
         dt = time.perf_counter() - t0
         k = out[6]
+        prec = "fp32 (MATLAB single rules)" if D.dtype == np.float32 else "fp64"
         return {"value": k / dt, "unit": "iters/s", "cores": threads, "kind": "port",
-                "sample": "%d ADMM iterations of the same %dx%dx%d r=%d fp64 workload "
+                "sample": "%d ADMM iterations of the same %dx%dx%d r=%d %s workload "
                           "(C restatement of triple_decomp_ADMM.m with its materialised "
                           "permutes/design matrices, GEMM and pinv; OpenMP; includes per-call "
-                          "setup)" % (k, *D.shape, r),
+                          "setup)" % (k, *D.shape, r, prec),
                 "seconds": dt}
     except Exception as e:  # the baseline is reported, never the product
         return {"value": None, "unit": "iters/s", "cores": 0, "kind": "port",
                 "sample": "unavailable: %s" % e}
 
 
-def pmc_traffic():
+def pmc_traffic(config):
     """HBM bytes per fused-update launch from the committed rocprofv3 PMC pass
-    (tools/pmc_traffic.py -> profiles/*_k5_traffic.json), or None."""
+    (tools/pmc_traffic.py -> profiles/*_k5_traffic.json, config 5:
+    profiles/*_c5_k5_traffic.json), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*k5_traffic.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*k5_traffic.json"))
+                   if ("_c5_" in os.path.basename(f)) == (config == 5))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -77,9 +83,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=N_DEFAULT)
-    ap.add_argument("--r", type=int, default=R_DEFAULT)
-    ap.add_argument("--cpu-iters", type=int, default=40)  # ~20 s of host work
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None, help="config 4: cube side override")
+    ap.add_argument("--r", type=int, default=None)
+    # bounded host sample: ~20 s at config 4, one iteration at config 5 (§8d)
+    ap.add_argument("--cpu-iters", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -104,24 +112,34 @@ def main():
     import tritd
     from tritd import synth
 
-    n, r = args.n, args.r
+    n1, n2, n3, r, dts = CONFIGS[args.config]
+    if args.n is not None:
+        if args.config != 4:
+            raise SystemExit("--n applies to config 4 (n^3)")
+        n1 = n2 = n3 = args.n
+    r = args.r if args.r is not None else r
+    f32 = dts == "f32"
+    npdt = np.float32 if f32 else np.float64
+    cpu_iters = args.cpu_iters if args.cpu_iters is not None else (1 if f32 else 40)
     K, W = args.steps, args.warmup
     maxIter = max(100, K + W)
     opts = dict(synth.TRAFFIC_OPTS, maxIter=maxIter, tol=synth.TRAFFIC_OPTS["tol"])
-    data = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
-    D, Lstar = data["D"], data["Lstar"]
+    # config 5 uses the same recipe, rounded to single
+    data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    D, Lstar = data["D"].astype(npdt, order="F"), data["Lstar"].astype(npdt, order="F")
+    del data["D"], data["Lstar"]
 
     # mode-1 shard of this rank
     from tritd.dist import make_comm, shard_bounds
-    i0, i1 = shard_bounds(n, world, rank)
+    i0, i1 = shard_bounds(n1, world, rank)
     comm = make_comm(dist, rank, world, local_rank) if world > 1 else None
 
     # inputs resident in HBM before the timed region
     dev = torch.device("cuda", local_rank)
     D_shard = torch.from_numpy(np.ascontiguousarray(D[i0:i1].transpose(2, 1, 0))).to(dev)
-    sess = tritd.Session(r, opts, data["A0"], data["B0"], data["C0"], n1=n, n2=n, n3=n, i0=i0,
+    sess = tritd.Session(r, opts, data["A0"], data["B0"], data["C0"], n1=n1, n2=n2, n3=n3, i0=i0,
                          i1=i1, d_device_ptr=D_shard.data_ptr(), ldD=i1 - i0, device=local_rank,
-                         comm=comm)
+                         comm=comm, dtype=npdt)
     del D_shard
 
     sess.run(W)
@@ -162,21 +180,39 @@ def main():
 
     # algorithmic bytes of the dominant kernel (fused update K5), per launch,
     # on this rank's shard: reads D, Y_L, Y_O + writes Y_L, Y_O,
-    # T (6 N-streams of 8 B; O is rebuilt on demand), E in compact form (one
-    # 256 B slot per 256-element tile read and written = 2 B per element),
-    # 4 KB per tile stored densely (more than 28 nonzeros; read next launch),
-    # and W (R * n1 * n2 doubles)
+    # T (6 N-streams of s bytes; O is rebuilt on demand), E in compact form
+    # (one 256 B slot per 256-element tile read and written), a whole tile
+    # (256 * s bytes) for each tile stored densely (read next launch), and W
+    # (R * n_local * n2 elements)
+    s_b = 4 if f32 else 8
     nl = i1 - i0
-    N_local = nl * n * n
-    k5_bytes = int(6 * N_local * 8 + 2 * tiles_per_launch * 256 + dense_per_launch * 4096
-                   + r * r * nl * n * 8)
+    N_local = nl * n2 * n3
+    tile_b = 256 * s_b
+    k5_bytes = int(6 * N_local * s_b + 2 * tiles_per_launch * 256 + dense_per_launch * tile_b
+                   + r * r * nl * n2 * s_b)
+    # flops: L(ij,t) = sum_k (Ah*Bh)(ij,k) Ch(t,k) and W = T x3 Ch, 2 N R each
+    k5_flops = 4.0 * N_local * r * r
     k5_ms = km["fused_update"]
-    achieved = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
-    traffic, traffic_src = pmc_traffic()
+    gbs = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
+    tfs = k5_flops / (k5_ms * 1e-3) / 1e12 if k5_ms > 0 else None
+    traffic, traffic_src = pmc_traffic(args.config)
+    if f32:  # config 5 is MFMA-bound
+        roof = {"bound": "mfma", "achieved": tfs, "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": (tfs / F32_MFMA_PEAK_TFS) if tfs else None,
+                "hbm_achieved_GBs": gbs, "hbm_frac": (gbs / HBM_PEAK_GBS) if gbs else None,
+                "algorithmic_flops_per_launch": k5_flops}
+    else:
+        roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
+                "mfma_achieved_TFs": tfs}
+    roof.update({"kernel": "k5_fused (fused ADMM update + L + W)", "traffic": traffic,
+                 "traffic_source": traffic_src, "algorithmic_bytes_per_launch": k5_bytes,
+                 "e_dense_tiles_per_launch": dense_per_launch,
+                 "e_tiles_per_launch": tiles_per_launch})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], args.cpu_iters)
+        cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], cpu_iters)
 
     if rank == 0:
         line = {
@@ -190,25 +226,19 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": dts,
             "data": "synthetic",
-            "config": {"workload": "synthetic %dx%dx%d fp64 r=%d low-rank + 5%% outliers "
+            "config": {"workload": "config %d: synthetic %dx%dx%d %s r=%d low-rank + 5%% outliers "
                                    "(SURVEY.md 8d), traffic opts (traffic_triple_comparison.m:42-50)"
-                                   % (n, n, n, r),
-                       "n1": n, "n2": n, "n3": n, "r": r, "maxIter": maxIter,
+                                   % (args.config, n1, n2, n3, "fp32" if f32 else "fp64", r),
+                       "n1": n1, "n2": n2, "n3": n3, "r": r, "maxIter": maxIter,
                        "parallelism": "mode1-shard x%d" % world},
             "rre_final": rre,
             "k_final": k_final,
             "errHist_final": errhist_final,
             "kernel_ms": {"fused_update": k5_ms, "mode3_mttkrp": km["mode3"],
                           "iteration_events": km["iteration"], "samples": km["samples"]},
-            "roofline": {"kernel": "k5_fused (fused ADMM update + L + W)", "bound": "hbm",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": k5_bytes,
-                         "e_dense_tiles_per_launch": dense_per_launch,
-                         "e_tiles_per_launch": tiles_per_launch},
+            "roofline": roof,
             "cpu_baseline": cpu,
             # candidate tensor pools timed with K5's access pattern at session
             # creation (rank 0), the fastest kept

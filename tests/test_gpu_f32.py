@@ -133,3 +133,25 @@ def test_f32_zero_iterations(tritd):
                                               d["B0"], d["C0"])
     assert len(eh) == 0 and not np.any(O) and O.dtype == np.float32
     np.testing.assert_array_equal(A, d["A0"])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_non_recovering_shape_rre_matches_oracle(tritd, cref, dtype):
+    """At 256x256x32 r=4 the reference's ADMM does not recover L* within
+    maxIter = 100 (RRE 0.24 in the C restatement, fp64 and fp32 alike): the
+    config-5 bench's RRE of 0.10 is the algorithm's, not the kernels'.  The
+    GPU reproduces the restatement's RRE to the stated tolerance."""
+    import tritd_oracle as orc
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(256, 256, 32, 4, p_out=0.05, seed=0, init_seed=123)
+    opts = dict(synth.TRAFFIC_OPTS)
+    mod, lib = cref
+    D = d["D"].astype(dtype)
+    ref = mod.admm(lib, D, 4, opts, d["A0"], d["B0"], d["C0"])
+    A, B, C, O, eh = tritd.triple_decomp_ADMM(D, 4, opts, d["A0"], d["B0"], d["C0"])
+    nL = np.linalg.norm(d["Lstar"])
+    rre = np.linalg.norm(orc.triple_product(A, B, C) - d["Lstar"]) / nL
+    rre_ref = np.linalg.norm(orc.triple_product(ref[0], ref[1], ref[2]) - d["Lstar"]) / nL
+    assert len(eh) == ref[6] == 100
+    assert rre_ref > 0.1
+    assert abs(rre - rre_ref) <= (1e-9 if dtype == np.float64 else 1e-4) * rre_ref

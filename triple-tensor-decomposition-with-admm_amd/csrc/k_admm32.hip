@@ -132,8 +132,12 @@ void k5_f32(K5Args32 a) {
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
 
-    __shared__ float sCT[2][RP * 16];   // [k][16]: L operand C^(t0 + l&15, 4s + (l>>4))
-    __shared__ float sC[2][16 * LDC];   // [t][k]:  W operand C^(t0 + 4(l>>4) + r, 16m + (l&15))
+    // C^ slice of the t-tile, [t][k] rows of stride LDC: the W operand reads
+    // C^(t0 + 4(l>>4) + r, 16m + (l&15)); the L operand's K index is renumbered
+    // k = (l>>4) * KS + s, so lane l walks its row t0 + (l&15) contiguously and
+    // reads four K-steps per ds_read_b128 (row offsets il * LDC put the 16
+    // lanes of a group on distinct banks for every RP)
+    __shared__ __attribute__((aligned(16))) float sC[2][16 * LDC];
     __shared__ float tsm[K5W][16 * 17]; // per-wave T transpose
     __shared__ float csm[K5W][128];     // per-wave compact-E slot image
     float* ts = tsm[wid];
@@ -158,20 +162,16 @@ void k5_f32(K5Args32 a) {
             const int e = threadIdx.x + q * 64 * K5W;
             if (SQ % (64 * K5W) == 0 || e < SQ) {
                 const int row = (4 * e) / RP, k = (4 * e) % RP;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    sC[buf][row * LDC + k + c] = sv[q][c];
-                    sCT[buf][(k + c) * 16 + row] = sv[q][c];
-                }
+                *reinterpret_cast<f4*>(&sC[buf][row * LDC + k]) = sv[q];
             }
         }
     };
 
-    float kr[KS];  // L operand KR(ij = l & 15, k = 4s + (l>>4)), single-rounded
+    float kr[KS];  // L operand KR(ij = l & 15, k = (l>>4) * KS + s), single-rounded
     if (!PRO) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            const int k = 4 * s + tg;
+            const int k = tg * KS + s;
             kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
         }
     }
@@ -225,7 +225,6 @@ void k5_f32(K5Args32 a) {
             for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
             if (pf) load_slot(tt + 2, cx.ce);
         }
-        const float* cT = sCT[buf];
         const float* cR = sC[buf];
         float tr[4];
         if (PRO) {
@@ -238,9 +237,14 @@ void k5_f32(K5Args32 a) {
             f4 lacc[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+            const f4* cL = reinterpret_cast<const f4*>(cR + il * LDC + tg * KS);
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
-                lacc[s & 3] = mfma32(cT[(4 * s + tg) * 16 + il], kr[s], lacc[s & 3]);
+            for (int s4 = 0; s4 < KS / 4; ++s4) {
+                const f4 c = cL[s4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+            }
             const f4 Lv = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
             float En[4];
             f4 YLn, YOn;
