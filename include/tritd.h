@@ -88,7 +88,8 @@ tritd_status tritd_device_count(int32_t* count);
  *   A,B,C   : outputs, reference layout
  *   O, E    : outputs, n1*n2*n3 (E is the 6th, extra output; may be NULL)
  *   errHist : capacity maxIter; *iters receives k (errHist = errHist(1:k), :68)
- * Runs on `device` (-1 = current/0).
+ * Runs on `device`; device = -1 runs on the device set of tritd_set_devices
+ * (the current device when none is set).
  * ------------------------------------------------------------------------- */
 tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3, int32_t r,
                             const tritd_opts* opts, const double* A0, const double* B0,
@@ -173,9 +174,23 @@ tritd_status tritd_comm_create(tritd_comm** out, const void* id128, int32_t nran
                                int32_t device);
 void tritd_comm_destroy(tritd_comm* c);
 
+/* Device set of the one-shot entry points (the MEX host
+ * drives every GPU from its one thread).  With n > 1, tritd_admm_{f64,f32}
+ * (device = -1) shard D along mode 1 over the set and run
+ * every iteration's phases on all shards from the calling thread; the three
+ * reductions per iteration are grouped ncclAllReduce calls over
+ * communicators from ncclCommInitAll (distinct devices), cached until the set
+ * changes or tritd_shutdown.  One device repeated n times runs n virtual
+ * shards on it (in-device sums).  n = 0 clears the set.  Replaces the
+ * reference's single-process CPU call (triple_decomp_ADMM.m:1) for data that
+ * exceeds one GPU. */
+tritd_status tritd_set_devices(const int32_t* devices, int32_t n);
+/* Frees the cached communicators and clears the device set (mexAtExit). */
+void tritd_shutdown(void);
+
 /* Single-GPU rehearsal of the sharded path: `nshards` sessions on one device
- * whose all-reduces are summed on the device in shard order.  Used by the
- * parity tests to check the mode-1 sharding on a 1-GPU box. */
+ * whose all-reduces are summed on the device in shard order (the device set
+ * {device} x nshards).  Used by the parity tests on a 1-GPU box. */
 tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
                                             int32_t r, const tritd_opts* opts, const double* A0,
                                             const double* B0, const double* C0, int32_t nshards,

@@ -10,7 +10,7 @@
 #include <string>
 
 typedef size_t mwSize;
-typedef enum { mxDOUBLE_CLASS, mxCHAR_CLASS, mxSTRUCT_CLASS } mxClassID;
+typedef enum { mxDOUBLE_CLASS, mxSINGLE_CLASS, mxCHAR_CLASS, mxSTRUCT_CLASS } mxClassID;
 typedef enum { mxREAL, mxCOMPLEX } mxComplexity;
 struct mxArray;
 
@@ -20,6 +20,7 @@ struct MockMexError {
 
 bool mxIsStruct(const mxArray*);
 bool mxIsDouble(const mxArray*);
+bool mxIsSingle(const mxArray*);
 bool mxIsComplex(const mxArray*);
 bool mxIsChar(const mxArray*);
 mxArray* mxGetField(const mxArray*, size_t, const char*);
@@ -28,6 +29,7 @@ mwSize mxGetNumberOfDimensions(const mxArray*);
 const mwSize* mxGetDimensions(const mxArray*);
 size_t mxGetNumberOfElements(const mxArray*);
 double* mxGetPr(const mxArray*);
+void* mxGetData(const mxArray*);
 void mxSetM(mxArray*, mwSize);
 int mxGetString(const mxArray*, char*, mwSize);
 mxArray* mxCreateNumericArray(mwSize, const mwSize*, mxClassID, mxComplexity);
@@ -35,4 +37,5 @@ mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
 void mxDestroyArray(mxArray*);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
 int mexPrintf(const char* fmt, ...);
+int mexAtExit(void (*fn)(void));
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]);

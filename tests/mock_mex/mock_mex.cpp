@@ -9,7 +9,8 @@
 struct mxArray {
     mxClassID cls = mxDOUBLE_CLASS;
     std::vector<mwSize> dims;
-    std::vector<double> data;
+    std::vector<double> data;  // mxDOUBLE_CLASS
+    std::vector<float> fdata;  // mxSINGLE_CLASS
     std::string str;
     std::map<std::string, mxArray*> fields;
 };
@@ -18,6 +19,7 @@ static std::string g_printed;
 
 bool mxIsStruct(const mxArray* a) { return a->cls == mxSTRUCT_CLASS; }
 bool mxIsDouble(const mxArray* a) { return a->cls == mxDOUBLE_CLASS; }
+bool mxIsSingle(const mxArray* a) { return a->cls == mxSINGLE_CLASS; }
 bool mxIsComplex(const mxArray*) { return false; }
 bool mxIsChar(const mxArray* a) { return a->cls == mxCHAR_CLASS; }
 mxArray* mxGetField(const mxArray* a, size_t, const char* n) {
@@ -33,6 +35,10 @@ size_t mxGetNumberOfElements(const mxArray* a) {
     return n;
 }
 double* mxGetPr(const mxArray* a) { return const_cast<double*>(a->data.data()); }
+void* mxGetData(const mxArray* a) {
+    return a->cls == mxSINGLE_CLASS ? static_cast<void*>(const_cast<float*>(a->fdata.data()))
+                                    : static_cast<void*>(const_cast<double*>(a->data.data()));
+}
 void mxSetM(mxArray* a, mwSize m) { a->dims[0] = m; }
 int mxGetString(const mxArray* a, char* buf, mwSize n) {
     std::snprintf(buf, n, "%s", a->str.c_str());
@@ -42,7 +48,10 @@ mxArray* mxCreateNumericArray(mwSize nd, const mwSize* d, mxClassID c, mxComplex
     auto* a = new mxArray;
     a->cls = c;
     a->dims.assign(d, d + nd);
-    a->data.assign(mxGetNumberOfElements(a), 0.0);
+    if (c == mxSINGLE_CLASS)
+        a->fdata.assign(mxGetNumberOfElements(a), 0.0f);
+    else
+        a->data.assign(mxGetNumberOfElements(a), 0.0);
     return a;
 }
 mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity c) {
@@ -71,6 +80,18 @@ int mexPrintf(const char* fmt, ...) {
     return n;
 }
 
+static void (*g_at_exit)(void) = nullptr;
+int mexAtExit(void (*fn)(void)) {
+    g_at_exit = fn;
+    return 0;
+}
+
+static mxArray* sgl(const float* p, std::vector<mwSize> dims) {
+    mxArray* a = mxCreateNumericArray(dims.size(), dims.data(), mxSINGLE_CLASS, mxREAL);
+    std::memcpy(a->fdata.data(), p, a->fdata.size() * sizeof(float));
+    return a;
+}
+
 static mxArray* dbl(const double* p, std::vector<mwSize> dims) {
     mxArray* a = mxCreateNumericArray(dims.size(), dims.data(), mxDOUBLE_CLASS, mxREAL);
     std::memcpy(a->data.data(), p, a->data.size() * sizeof(double));
@@ -78,18 +99,48 @@ static mxArray* dbl(const double* p, std::vector<mwSize> dims) {
 }
 
 extern "C" {
-// opt_names: comma-separated field names present in opts; opt_vals in the same order
-int mock_admm(const double* D, long n1, long n2, long n3, int r, const char* opt_names,
-              const double* opt_vals, const double* A0, const double* B0, const double* C0,
-              double* A, double* B, double* C, double* O, double* E, double* errHist, int* k,
-              char* err, int errlen, char* printed, int printlen) {
-    std::vector<mxArray*> in;
+static mxArray* cmd_arg(const char* c) {
     auto* cmd = new mxArray;
     cmd->cls = mxCHAR_CLASS;
-    cmd->str = "admm";
-    cmd->dims = {1, 4};
-    in.push_back(cmd);
-    in.push_back(dbl(D, {(mwSize)n1, (mwSize)n2, (mwSize)n3}));
+    cmd->str = c;
+    cmd->dims = {1, std::strlen(c)};
+    return cmd;
+}
+
+// tritd_mex('devices', devs) (n = 0: an empty matrix); returns 0 or 1 + err
+int mock_devices(const double* devs, int n, char* err, int errlen) {
+    mxArray* in[2] = {cmd_arg("devices"), dbl(devs, {1, (mwSize)n})};
+    int rc = 0;
+    try {
+        mexFunction(0, nullptr, 2, const_cast<const mxArray**>(in));
+    } catch (const MockMexError& e) {
+        std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
+        rc = 1;
+    }
+    for (auto* a : in) mxDestroyArray(a);
+    return rc;
+}
+
+// MATLAB clearing the MEX: runs the function registered with mexAtExit
+int mock_clear(void) {
+    if (!g_at_exit) return 1;
+    g_at_exit();
+    g_at_exit = nullptr;
+    return 0;
+}
+
+// opt_names: comma-separated field names present in opts; opt_vals in the same order.
+// single != 0: D, O, E are float (a D of class single).
+int mock_admm(const void* D, long n1, long n2, long n3, int r, const char* opt_names,
+              const double* opt_vals, const double* A0, const double* B0, const double* C0,
+              double* A, double* B, double* C, void* O, void* E, double* errHist, int* k,
+              char* err, int errlen, char* printed, int printlen, int single) {
+    std::vector<mxArray*> in;
+    in.push_back(cmd_arg("admm"));
+    if (single)
+        in.push_back(sgl(static_cast<const float*>(D), {(mwSize)n1, (mwSize)n2, (mwSize)n3}));
+    else
+        in.push_back(dbl(static_cast<const double*>(D), {(mwSize)n1, (mwSize)n2, (mwSize)n3}));
     double rr = r;
     in.push_back(dbl(&rr, {1, 1}));
     auto* opts = new mxArray;
@@ -121,10 +172,13 @@ int mock_admm(const double* D, long n1, long n2, long n3, int r, const char* opt
         std::memcpy(A, out[0]->data.data(), nA * 8);
         std::memcpy(B, out[1]->data.data(), nB * 8);
         std::memcpy(C, out[2]->data.data(), nC * 8);
-        std::memcpy(O, out[3]->data.data(), N * 8);
+        const size_t es = single ? 4 : 8;
+        if ((out[3]->cls == mxSINGLE_CLASS) != (single != 0) || (out[5]->cls == mxSINGLE_CLASS) != (single != 0))
+            throw MockMexError{"mock:class", "O/E class differs from the class of D"};
+        std::memcpy(O, mxGetData(out[3]), N * es);
         *k = (int)out[4]->dims[0];
         std::memcpy(errHist, out[4]->data.data(), (size_t)*k * 8);
-        std::memcpy(E, out[5]->data.data(), N * 8);
+        std::memcpy(E, mxGetData(out[5]), N * es);
     } catch (const MockMexError& e) {
         std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
         rc = 1;

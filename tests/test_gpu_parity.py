@@ -81,6 +81,51 @@ def test_virtual_shards_match_golden(tritd, orc, name, P):
     check_solution(orc, got, g, g["k"])
 
 
+@pytest.mark.parametrize("name,P", [("g30_r3", 3), ("g54x4x96_r5_sensor", 2)])
+def test_device_set_matches_golden(tritd, orc, name, P):
+    """tritd_set_devices: one GPU repeated P times drives the
+    sharded schedule of the single-process multi-GPU path from this thread."""
+    g = load_golden(name)
+    tritd.set_devices([0] * P)
+    try:
+        got = tritd.triple_decomp_ADMM(g["D"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                       return_E=True, return_iters=True)
+    finally:
+        tritd.set_devices([])
+    check_solution(orc, got, g, g["k"])
+
+
+def test_device_set_f32_and_errors(tritd, orc):
+    """The fp32 path over a device set matches its single-device run; a set
+    naming an absent device, or mixing repeats with other devices, fails
+    like the reference's argument errors (nothing runs)."""
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(40, 24, 36, 3, seed=5, init_seed=9)
+    D = d["D"].astype(np.float32)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=25)
+    one = tritd.triple_decomp_ADMM(D, 3, opts, d["A0"], d["B0"], d["C0"], return_E=True,
+                                   return_iters=True)
+    tritd.set_devices([0, 0])
+    try:
+        two = tritd.triple_decomp_ADMM(D, 3, opts, d["A0"], d["B0"], d["C0"], return_E=True,
+                                       return_iters=True)
+    finally:
+        tritd.set_devices([])
+    assert one[6] == two[6] and two[3].dtype == np.float32
+    assert rel(orc.triple_product(*two[:3]), orc.triple_product(*one[:3])) <= 1e-5
+    assert rel(two[3].astype(np.float64), one[3].astype(np.float64)) <= 1e-5
+    n = tritd.device_count()
+    with pytest.raises(tritd.TritdError):
+        tritd.set_devices([n])
+    if n >= 2:
+        tritd.set_devices([0, 0, 1])
+        try:
+            with pytest.raises(tritd.TritdError, match="distinct devices or one device repeated"):
+                tritd.triple_decomp_ADMM(D, 3, opts, d["A0"], d["B0"], d["C0"])
+        finally:
+            tritd.set_devices([])
+
+
 def test_medium_against_oracle(tritd, orc):
     """A size with several workgroups per kernel and ragged padding."""
     from tritd import synth

@@ -27,8 +27,8 @@ def gw(tmp_path_factory):
     return lib
 
 
-def run(gw, g, names=None, vals=None):
-    D = np.asfortranarray(g["D"])
+def run(gw, g, names=None, vals=None, single=False):
+    D = np.asfortranarray(g["D"], dtype=np.float32 if single else np.float64)
     n1, n2, n3 = D.shape
     r = g["r"]
     o = g["opts"]
@@ -46,7 +46,8 @@ def run(gw, g, names=None, vals=None):
     p = lambda a: C.c_void_p(a.ctypes.data)
     A0, B0, C0 = (np.asfortranarray(g[x]) for x in ("A0", "B0", "C0"))
     rc = gw.mock_admm(p(D), n1, n2, n3, r, ",".join(names).encode(), p(vals), p(A0), p(B0), p(C0),
-                      p(A), p(B), p(Cc), p(O), p(E), p(eh), C.byref(k), err, 1024, pr, 4096)
+                      p(A), p(B), p(Cc), p(O), p(E), p(eh), C.byref(k), err, 1024, pr, 4096,
+                      int(single))
     return rc, err.value.decode(), dict(A=A, B=B, C=Cc, O=O, E=E, errHist=eh[: k.value], k=k.value,
                                         printed=pr.value.decode())
 
@@ -88,3 +89,43 @@ def test_gateway_disp_goes_through_mexPrintf(gw):
     rc, err, res = run(gw, g)
     assert rc == 0, err
     assert res["printed"].splitlines()[0].startswith("Iter 10, errL=")
+
+
+def devices(gw, idx):
+    err = C.create_string_buffer(1024)
+    v = np.asarray(idx, dtype=np.float64)
+    rc = gw.mock_devices(C.c_void_p(v.ctypes.data) if len(v) else None, len(v), err, 1024)
+    return rc, err.value.decode()
+
+
+def test_gateway_devices_validates(gw):
+    rc, err = devices(gw, [0.5])
+    assert rc == 1 and err == "tritd:devices|device ordinals must be integers"
+    rc, err = devices(gw, list(range(17)))
+    assert rc == 1 and err == "tritd:devices|at most 16 devices"
+    rc, err = devices(gw, [])  # clearing the set needs no GPU
+    assert rc == 0, err
+    assert gw.mock_clear() == 0  # the gateway registered tritd_shutdown with mexAtExit
+
+
+@pytest.mark.gpu
+def test_gateway_single_class_and_device_set(gw):
+    """A single D goes through tritd_admm_f32 with single O/E; a device set of
+    one GPU repeated twice runs the sharded schedule (virtual shards)."""
+    import tritd_oracle as orc
+    g = load_golden("g30_r3")
+    rc, err, one = run(gw, g, single=True)
+    assert rc == 0, err
+    assert one["O"].dtype == np.float32 and one["k"] == g["k"]
+    assert rel(orc.triple_product(one["A"], one["B"], one["C"]),
+               orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-4
+    rc, err = devices(gw, [0, 0])
+    assert rc == 0, err
+    try:
+        rc, err, two = run(gw, g)
+        assert rc == 0, err
+        assert two["k"] == g["k"]
+        assert rel(two["O"], g["O"]) <= 1e-9
+        np.testing.assert_allclose(two["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
+    finally:
+        assert devices(gw, [])[0] == 0

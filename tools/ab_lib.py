@@ -18,7 +18,14 @@ for p in paths:
         fn = getattr(l, name); fn.restype = res; fn.argtypes = args
     libs[p] = l
 n, r = 512, 8
-if os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere (worst case for CE)
+n1 = n2 = n3 = n
+cfg5 = os.environ.get("AB_CFG", "4") == "5"
+if cfg5:  # 2048x2048x256 r=16 fp32 (bench.py --config 5)
+    n1, n2, n3, r = 2048, 2048, 256, 16
+    dd = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    D, A0, B0, C0 = dd["D"].astype(np.float32, order="F"), dd["A0"], dd["B0"], dd["C0"]
+    del dd
+elif os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere (worst case for CE)
     rng = np.random.default_rng(0)
     D = np.asfortranarray(rng.standard_normal((n, n, n)))
     A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
@@ -31,7 +38,7 @@ res = {p: [] for p in paths}
 for rep in range(reps):
     for p in paths:
         api.lib = _lib.lib = libs[p]
-        s = tritd.Session(r, opts, A0, B0, C0, n1=n, n2=n, n3=n, D=D, device=0)
+        s = tritd.Session(r, opts, A0, B0, C0, n1=n1, n2=n2, n3=n3, D=D, device=0)
         s.run(warm); s.sync(); s.set_timing(True); s.run(iters); s.sync()
         km = s.kernel_ms()
         pr = s.probe() if hasattr(libs[p], "tritd_session_probe") else None

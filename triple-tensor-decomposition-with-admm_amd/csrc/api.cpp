@@ -85,6 +85,130 @@ int pick_device(int32_t device) {
 }
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Device set of the one-shot entry points (tritd_set_devices), and the RCCL
+// communicators of a set of distinct devices (ncclCommInitAll): created on
+// first use, kept in this process-global context until the set changes or
+// tritd_shutdown (SURVEY.md §8b Ownership).
+std::vector<int> g_devices;
+std::vector<int> g_comm_devs;
+std::vector<ncclComm_t> g_comms;
+
+void drop_comms() {
+    for (ncclComm_t c : g_comms)
+        if (c) (void)ncclCommDestroy(c);
+    g_comms.clear();
+    g_comm_devs.clear();
+}
+
+void group_comms(const std::vector<int>& devs) {
+    if (g_comm_devs == devs && !g_comms.empty()) return;
+    drop_comms();
+    g_comms.assign(devs.size(), nullptr);
+    const ncclResult_t r = ncclCommInitAll(g_comms.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) {
+        g_comms.clear();
+        throw Error(TRITD_ERR_RCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    }
+    g_comm_devs = devs;
+}
+
+// One problem sharded along mode 1 over `devs`, driven from
+// the calling thread (§8b Threading): every iteration runs the four phases of
+// solver.cpp on each shard, and the three reductions between them are one
+// grouped ncclAllReduce per buffer over the shards' streams (distinct
+// devices), or an in-device sum of the shards' buffers when one device is
+// repeated (virtual shards: the sharded schedule on one GPU).  D, O, E are
+// column-major n1 x n2 x n3 host arrays of es-byte elements.
+void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t flags, int64_t n1,
+               int64_t n2, int64_t n3, int32_t r, const tritd_opts& o, const double* A0,
+               const double* B0, const double* C0, double* A, double* B, double* C, void* O,
+               void* E, double* errHist, int32_t* iters) {
+    const int P = (int)devs.size();
+    if (P < 1 || P > 16) throw Error(TRITD_ERR_ARG, "a device set holds 1..16 devices");
+    if (P > n1) throw Error(TRITD_ERR_ARG, "more shards than mode-1 rows");
+    bool same = true, distinct = true;
+    for (int p = 0; p < P; ++p) {
+        if (devs[p] != devs[0]) same = false;
+        for (int q = 0; q < p; ++q)
+            if (devs[p] == devs[q]) distinct = false;
+    }
+    if (!same && !distinct)
+        throw Error(TRITD_ERR_ARG, "a device set is distinct devices or one device repeated");
+    for (int d : devs) pick_device(d);
+    if (distinct && P > 1) group_comms(devs);
+
+    hipStream_t vst = nullptr;  // the shared stream of virtual shards
+    struct StreamGuard {
+        hipStream_t s = nullptr;
+        ~StreamGuard() {
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } sg;
+    if (same && P > 1) {
+        TRITD_HIP(hipSetDevice(devs[0]));
+        TRITD_HIP(hipStreamCreateWithFlags(&vst, hipStreamNonBlocking));
+        sg.s = vst;
+    }
+    std::vector<std::unique_ptr<Session>> ss;
+    for (int p = 0; p < P; ++p) {  // balanced rows: every shard non-empty
+        const int64_t i0 = n1 * p / P, i1 = n1 * (p + 1) / P;
+        TRITD_HIP(hipSetDevice(devs[p]));
+        ss.emplace_back(new Session(devs[p], static_cast<const char*>(D) + i0 * es, n1, n1, n2, n3,
+                                    i0, i1, r, o, A0, B0, C0, nullptr, flags, vst,
+                                    /*defer_normD=*/true));
+    }
+    std::vector<double*> b(P);
+    auto reduce = [&](double* (Session::*get)(), int64_t count) {
+        if (P == 1) return;
+        for (int p = 0; p < P; ++p) b[p] = ((*ss[p]).*get)();
+        if (same) {
+            launch_vsum(b.data(), P, count, vst);
+            return;
+        }
+        ncclResult_t rr = ncclGroupStart();
+        for (int p = 0; p < P && rr == ncclSuccess; ++p) {
+            TRITD_HIP(hipSetDevice(devs[p]));
+            rr = ncclAllReduce(b[p], b[p], (size_t)count, ncclFloat64, ncclSum, g_comms[p],
+                               ss[p]->stream());
+        }
+        const ncclResult_t re = ncclGroupEnd();
+        if (rr != ncclSuccess || re != ncclSuccess)
+            throw Error(TRITD_ERR_RCCL, std::string("grouped ncclAllReduce: ") +
+                                            ncclGetErrorString(rr != ncclSuccess ? rr : re));
+    };
+    auto each = [&](auto&& f) {
+        for (auto& s : ss) {
+            TRITD_HIP(hipSetDevice(s->device()));
+            f(*s);
+        }
+    };
+    reduce(&Session::red3, 2);
+    each([](Session& s) { s.set_normD_from_red3(); });
+    for (int it = 0; it < o.maxIter; ++it) {
+        int k = 0;
+        each([&](Session& s) { k = s.next_iter(); });
+        if (!k) break;
+        each([&](Session& s) { s.phaseA(k); });
+        reduce(&Session::red1, ss[0]->red1_count());
+        each([&](Session& s) { s.phaseB(k); });
+        reduce(&Session::red2, ss[0]->red2_count());
+        each([&](Session& s) { s.phaseC(k); });
+        reduce(&Session::red3, 2);
+        each([&](Session& s) { s.phaseD(k); });
+        TRITD_HIP(hipSetDevice(devs[0]));
+        ss[0]->maybe_print(k);
+    }
+    int k = 0;
+    for (int p = 0; p < P; ++p) {
+        const int64_t i0 = ss[p]->geom().i0;
+        TRITD_HIP(hipSetDevice(devs[p]));
+        ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr,
+                   O ? static_cast<char*>(O) + i0 * es : nullptr,
+                   E ? static_cast<char*>(E) + i0 * es : nullptr, n1, p == 0 ? errHist : nullptr, &k);
+    }
+    if (iters) *iters = k;
+}
 }  // namespace
 
 namespace tritd {
@@ -126,8 +250,13 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
         check_opts(opts);
         check_dims(n1, n2, n3, r);
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
-        const int dev = pick_device(device);
         const tritd_opts o = normalized(opts);
+        if (device < 0 && g_devices.size() > 1) {
+            run_group(g_devices, D, sizeof(double), 0, n1, n2, n3, r, o, A0, B0, C0, A, B, C, O, E,
+                      errHist, iters);
+            return;
+        }
+        const int dev = pick_device(device < 0 && !g_devices.empty() ? g_devices[0] : device);
         Session s(dev, D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, 0);
         s.run(o.maxIter);
         int k = 0;
@@ -145,8 +274,13 @@ tritd_status tritd_admm_f32(const float* D, int64_t n1, int64_t n2, int64_t n3, 
         check_opts(opts);
         check_dims(n1, n2, n3, r, true);
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
-        const int dev = pick_device(device);
         const tritd_opts o = normalized(opts);
+        if (device < 0 && g_devices.size() > 1) {
+            run_group(g_devices, D, sizeof(float), TRITD_SESSION_F32, n1, n2, n3, r, o, A0, B0, C0,
+                      A, B, C, O, E, errHist, iters);
+            return;
+        }
+        const int dev = pick_device(device < 0 && !g_devices.empty() ? g_devices[0] : device);
         Session s(dev, D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, TRITD_SESSION_F32);
         s.run(o.maxIter);
         int k = 0;
@@ -324,50 +458,30 @@ tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
         if (nshards < 1 || nshards > 16 || nshards > n1) throw Error(TRITD_ERR_ARG, "nshards must be in 1..min(16,n1)");
         const int dev = pick_device(device);
-        const tritd_opts o = normalized(opts);
-        hipStream_t st;
-        TRITD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-        struct StreamGuard {
-            hipStream_t s;
-            ~StreamGuard() { (void)hipStreamDestroy(s); }
-        } sg{st};
-        std::vector<std::unique_ptr<Session>> ss;
-        const int64_t chunk = (n1 + nshards - 1) / nshards;
-        for (int p = 0; p < nshards; ++p) {
-            const int64_t i0 = p * chunk, i1 = std::min<int64_t>(n1, i0 + chunk);
-            if (i0 >= i1) break;
-            ss.emplace_back(new Session(dev, D + i0, n1, n1, n2, n3, i0, i1, r, o, A0, B0, C0, nullptr,
-                                        0, st, /*defer_normD=*/true));
-        }
-        const int P = (int)ss.size();
-        std::vector<double*> b(P);
-        auto vsum = [&](double* (Session::*get)(), int64_t count) {
-            for (int p = 0; p < P; ++p) b[p] = ((*ss[p]).*get)();
-            launch_vsum(b.data(), P, count, st);
-        };
-        vsum(&Session::red3, 2);
-        for (auto& s : ss) s->set_normD_from_red3();
-        for (int it = 0; it < o.maxIter; ++it) {
-            int k = 0;
-            for (auto& s : ss) k = s->next_iter();
-            if (!k) break;
-            for (auto& s : ss) s->phaseA(k);
-            vsum(&Session::red1, ss[0]->red1_count());
-            for (auto& s : ss) s->phaseB(k);
-            vsum(&Session::red2, ss[0]->red2_count());
-            for (auto& s : ss) s->phaseC(k);
-            vsum(&Session::red3, 2);
-            for (auto& s : ss) s->phaseD(k);
-            ss[0]->maybe_print(k);
-        }
-        int k = 0;
-        for (int p = 0; p < P; ++p) {
-            const int64_t i0 = ss[p]->geom().i0;
-            ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, O ? O + i0 : nullptr,
-                       E ? E + i0 : nullptr, n1, p == 0 ? errHist : nullptr, &k);
-        }
-        if (iters) *iters = k;
+        run_group(std::vector<int>(nshards, dev), D, sizeof(double), 0, n1, n2, n3, r,
+                  normalized(opts), A0, B0, C0, A, B, C, O, E, errHist, iters);
     });
+}
+
+tritd_status tritd_set_devices(const int32_t* devices, int32_t n) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        if (n < 0 || n > 16) throw Error(TRITD_ERR_ARG, "a device set holds 0..16 devices");
+        if (n > 0) need(devices, "devices");
+        std::vector<int> d(devices, devices + n);
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+        for (int x : d)
+            if (x < 0 || x >= count) throw Error(TRITD_ERR_NODEV, "device index out of range");
+        if (d != g_comm_devs) drop_comms();
+        g_devices = d;
+    });
+}
+
+void tritd_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    drop_comms();
+    g_devices.clear();
 }
 
 // ---------------------------------------------------------------------------

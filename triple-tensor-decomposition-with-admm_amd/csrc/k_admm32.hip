@@ -19,6 +19,12 @@
 // nonzeros -> the tile is stored densely in E and its masks are all ones.
 #include "kernels.h"
 
+// K5F_EXP (timing experiments only, results invalid): 1 no W MFMAs, 2 no L
+// MFMAs, 3 no compact-E decode/encode, 4 no C^ staging
+#ifndef K5F_EXP
+#define K5F_EXP 0
+#endif
+
 namespace tritd {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -132,11 +138,20 @@ void k5_f32(K5Args32 a) {
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
 
-    // C^ slice of the t-tile, [t][k] rows of stride LDC: the W operand reads
-    // C^(t0 + 4(l>>4) + r, 16m + (l&15)); the L operand's K index is renumbered
-    // k = (l>>4) * KS + s, so lane l walks its row t0 + (l&15) contiguously and
-    // reads four K-steps per ds_read_b128 (row offsets il * LDC put the 16
-    // lanes of a group on distinct banks for every RP)
+    // C^ slice of the t-tile, [t][k] rows of stride LDC.  The L operand's K
+    // index is renumbered k = (l>>4) * KS + s, so lane l walks its row
+    // t0 + (l&15) contiguously and reads four K-steps per ds_read_b128 (row
+    // offsets il * LDC put the 16 lanes of a group on distinct banks).
+    // WB (RP % 64 == 0): W's M index is renumbered too, M-tile m row rho <->
+    // k = rho * MT + m, so lane l reads the MT contiguous k of chunk (l&15) of
+    // row t0 + 4(l>>4) + r with MT/4 ds_read_b128; inside each chunk of
+    // G = MT/4 16-byte granules, granule q sits at (q + (c*G >> 4)) mod G,
+    // which puts the 16 chunks a W read touches on 16 distinct bank groups
+    // and keeps the L reads conflict-free.  Otherwise W reads C^(t, 16m + l&15)
+    // one float per MFMA.
+    constexpr bool WB = RP % 64 == 0;
+    constexpr int G = WB ? MT / 4 : 1;
+    auto gran = [](int c, int q) { return c * G + ((q + ((c * G) >> 4)) & (G - 1)); };
     __shared__ __attribute__((aligned(16))) float sC[2][16 * LDC];
     __shared__ float tsm[K5W][16 * 17]; // per-wave T transpose
     __shared__ float csm[K5W][128];     // per-wave compact-E slot image
@@ -149,6 +164,7 @@ void k5_f32(K5Args32 a) {
     constexpr int NS = (SQ + 64 * K5W - 1) / (64 * K5W);
     f4 sv[NS];
     auto stage_load = [&](int64_t tt) {
+        if (K5F_EXP == 4) return;
         const f4* src = reinterpret_cast<const f4*>(a.ChF + (tt << 4) * RP);
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
@@ -157,12 +173,14 @@ void k5_f32(K5Args32 a) {
         }
     };
     auto stage_store = [&](int buf) {
+        if (K5F_EXP == 4) return;
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int e = threadIdx.x + q * 64 * K5W;
             if (SQ % (64 * K5W) == 0 || e < SQ) {
                 const int row = (4 * e) / RP, k = (4 * e) % RP;
-                *reinterpret_cast<f4*>(&sC[buf][row * LDC + k]) = sv[q];
+                const int kp = WB ? 4 * gran((k >> 2) / G, (k >> 2) % G) : k;
+                *reinterpret_cast<f4*>(&sC[buf][row * LDC + kp]) = sv[q];
             }
         }
     };
@@ -220,7 +238,8 @@ void k5_f32(K5Args32 a) {
         }
         float ev[4];
         if (!PRO) {
-            const bool dn = ce32_decode(cx.ce, lane, ev);
+            const bool dn = K5F_EXP == 3 ? false : ce32_decode(cx.ce, lane, ev);
+            if (K5F_EXP == 3) ev[0] = ev[1] = ev[2] = ev[3] = cx.ce;
 #pragma unroll
             for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
             if (pf) load_slot(tt + 2, cx.ce);
@@ -237,13 +256,17 @@ void k5_f32(K5Args32 a) {
             f4 lacc[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-            const f4* cL = reinterpret_cast<const f4*>(cR + il * LDC + tg * KS);
+            const f4* cL = reinterpret_cast<const f4*>(cR + il * LDC);
 #pragma unroll
             for (int s4 = 0; s4 < KS / 4; ++s4) {
-                const f4 c = cL[s4];
+                // logical granule tg * KS/4 + s4 of row il
+                const int gl = tg * (KS / 4) + s4;
+                const f4 c = cL[WB ? gran(gl / G, gl % G) : gl];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+                for (int u = 0; u < 4; ++u) {
+                    if (K5F_EXP == 2) lacc[u][0] += c[u] * kr[4 * s4 + u];
+                    else lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+                }
             }
             const f4 Lv = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
             float En[4];
@@ -270,7 +293,8 @@ void k5_f32(K5Args32 a) {
             }
             YL4[o] = YLn;
             YO4[o] = YOn;
-            ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), a.dense_tiles);
+            if (K5F_EXP == 3) a.CE[(tb >> 8) * CE32_SLOT + lane] = En[0] + En[1] + En[2] + En[3];
+            else ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), a.dense_tiles);
         }
         // T -> TX order through the wave's LDS tile: ts[t][ij]
 #pragma unroll
@@ -282,11 +306,28 @@ void k5_f32(K5Args32 a) {
         for (int s = 0; s < 4; ++s) tv[s] = ts[il * 17 + 4 * s + tg];
         T4[o] = tv;
         // W^T(k, ij) += sum_t C^(t,k) T(t,ij): K-step r covers t = 4(l>>4) + r
+        if (WB) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) {
+                const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
 #pragma unroll
-            for (int m = 0; m < MT; ++m)
-                wacc[m] = mfma32(cR[(4 * tg + r) * LDC + 16 * m + il], tr[r], wacc[m]);
+                for (int q = 0; q < G; ++q) {
+                    const f4 c = cW[gran(il, q)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (K5F_EXP == 1) wacc[4 * q + u][r] += c[u] * tr[r];
+                        else wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    if (K5F_EXP == 1) wacc[m][r] += cR[(4 * tg + r) * LDC + 16 * m + il] * tr[r];
+                    else wacc[m] = mfma32(cR[(4 * tg + r) * LDC + 16 * m + il], tr[r], wacc[m]);
+        }
         if (pf) stage_store(buf ^ 1);
         __syncthreads();
         __builtin_amdgcn_sched_barrier(0);
@@ -318,13 +359,17 @@ void k5_f32(K5Args32 a) {
         body(tt, 0, xa, xb, false);
     }
     if (active) {
-        // W^T C/D layout (f32): row k = 16m + 4(l>>4) + rr, col ij = l & 15
+        // W^T C/D layout (f32): M-tile m row rho = 4(l>>4) + rr, col ij = l & 15;
+        // k = rho * MT + m (WB) or 16m + rho
         const int64_t wbase = (tile << 4) + il;
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
-                a.Wk[(int64_t)(16 * m + 4 * tg + rr) * a.plane + wbase] = wacc[m][rr];
+            for (int rr = 0; rr < 4; ++rr) {
+                const int rho = 4 * tg + rr;
+                const int k = WB ? rho * MT + m : 16 * m + rho;
+                a.Wk[(int64_t)k * a.plane + wbase] = wacc[m][rr];
+            }
     }
     if (!PRO) {
 #pragma unroll

@@ -7,10 +7,16 @@ function [A, B, C, O, errHist, E] = triple_decomp_ADMM(D, r, opts)
 %
 %   The initial factors are drawn here with randn in the reference's order
 %   (A, then B, then C), so the global RNG stream and the starting point are
-%   those of the reference run.  D is processed in double precision.
+%   those of the reference run.  A single D keeps its class (the fp32 path:
+%   O and E single, A, B, C and errHist double, as MATLAB's class rules give
+%   the reference); any other class is processed in double.  Use
+%   tritd_devices(idx) to shard D over several GPUs.
 [n1, n2, n3] = size(D);
 A0 = randn(n1, r, r);
 B0 = randn(r, n2, r);
 C0 = randn(r, r, n3);
-[A, B, C, O, errHist, E] = tritd_mex('admm', double(D), r, opts, A0, B0, C0);
+if ~isa(D, 'single')
+    D = double(D);
+end
+[A, B, C, O, errHist, E] = tritd_mex('admm', D, r, opts, A0, B0, C0);
 end

@@ -1,6 +1,11 @@
 // tritd_mex.cpp — MATLAB MEX gateway over libtritd.so (include/tritd.h).
 //
 //   [A,B,C,O,errHist,E] = tritd_mex('admm', D, r, opts, A0, B0, C0)
+//                         D double -> tritd_admm_f64; D single -> tritd_admm_f32
+//                         (O, E single; A, B, C, errHist double: MATLAB's class
+//                         rules for a single D)
+//   tritd_mex('devices', idx)  HIP device ordinals (0-based) the next solves
+//                         shard D over (tritd_set_devices; [] clears)
 //   X  = tritd_mex('triple_product', A, B, C)
 //   Xn = tritd_mex('unfold', X, mode)
 //   Y  = tritd_mex('soft_threshold', X, lam)
@@ -75,10 +80,14 @@ bool size3(const mxArray* X, int64_t d[3], std::string* err) {
     return true;
 }
 
-mxArray* make3(int64_t a, int64_t b, int64_t c) {
+mxArray* make3(int64_t a, int64_t b, int64_t c, mxClassID cls = mxDOUBLE_CLASS) {
     const mwSize dims[3] = {(mwSize)a, (mwSize)b, (mwSize)c};
-    return mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
+    return mxCreateNumericArray(3, dims, cls, mxREAL);
 }
+
+// mexAtExit: the cached RCCL communicators go with the MEX (§8b Ownership)
+void at_exit() { tritd_shutdown(); }
+bool g_at_exit_set = false;
 
 [[noreturn]] void fail(const char* id, const std::string& msg) {
     mexErrMsgIdAndTxt(id, "%s", msg.c_str());
@@ -96,7 +105,8 @@ std::string status_msg(tritd_status s) {
 void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (nrhs != 7) fail("tritd:nargin", "usage: tritd_mex('admm', D, r, opts, A0, B0, C0)");
     const mxArray* D = prhs[1];
-    need_double(D, "D");
+    const bool single = mxIsSingle(D) && !mxIsComplex(D);
+    if (!single) need_double(D, "D");
     int64_t n[3];
     std::string err;
     if (!size3(D, n, &err)) fail("tritd:dims", err);
@@ -113,15 +123,21 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* A = make3(n[0], r, r);
     mxArray* B = make3(r, n[1], r);
     mxArray* C = make3(r, r, n[2]);
-    mxArray* O = make3(n[0], n[1], n[2]);
-    mxArray* E = make3(n[0], n[1], n[2]);
+    const mxClassID cls = single ? mxSINGLE_CLASS : mxDOUBLE_CLASS;
+    mxArray* O = make3(n[0], n[1], n[2], cls);
+    mxArray* E = make3(n[0], n[1], n[2], cls);
     mxArray* eh = mxCreateDoubleMatrix(o.maxIter > 0 ? o.maxIter : 0, 1, mxREAL);
     int32_t k = 0;
     tritd_set_print_callback(print_line, nullptr);
-    const tritd_status st = tritd_admm_f64(mxGetPr(D), n[0], n[1], n[2], r, &o, mxGetPr(prhs[4]),
-                                           mxGetPr(prhs[5]), mxGetPr(prhs[6]), mxGetPr(A),
-                                           mxGetPr(B), mxGetPr(C), mxGetPr(O), mxGetPr(E),
-                                           o.maxIter > 0 ? mxGetPr(eh) : nullptr, &k, -1);
+    double* ehp = o.maxIter > 0 ? mxGetPr(eh) : nullptr;
+    const tritd_status st =
+        single ? tritd_admm_f32(static_cast<const float*>(mxGetData(D)), n[0], n[1], n[2], r, &o,
+                                mxGetPr(prhs[4]), mxGetPr(prhs[5]), mxGetPr(prhs[6]), mxGetPr(A),
+                                mxGetPr(B), mxGetPr(C), static_cast<float*>(mxGetData(O)),
+                                static_cast<float*>(mxGetData(E)), ehp, &k, -1)
+               : tritd_admm_f64(mxGetPr(D), n[0], n[1], n[2], r, &o, mxGetPr(prhs[4]),
+                                mxGetPr(prhs[5]), mxGetPr(prhs[6]), mxGetPr(A), mxGetPr(B),
+                                mxGetPr(C), mxGetPr(O), mxGetPr(E), ehp, &k, -1);
     if (st != TRITD_OK) {
         for (mxArray* x : {A, B, C, O, E, eh}) mxDestroyArray(x);
         fail(st == TRITD_ERR_OPTS ? "MATLAB:nonExistentField" : "tritd:solver", status_msg(st));
@@ -134,6 +150,21 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         else
             mxDestroyArray(outs[q]);
     }
+}
+
+void do_devices(int, mxArray*[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs != 2) fail("tritd:nargin", "usage: tritd_mex('devices', idx)");
+    need_double(prhs[1], "idx");
+    const size_t n = mxGetNumberOfElements(prhs[1]);
+    if (n > 16) fail("tritd:devices", "at most 16 devices");
+    int32_t d[16];
+    const double* v = mxGetPr(prhs[1]);
+    for (size_t q = 0; q < n; ++q) {
+        if (v[q] != (double)(int32_t)v[q]) fail("tritd:devices", "device ordinals must be integers");
+        d[q] = (int32_t)v[q];
+    }
+    const tritd_status st = tritd_set_devices(d, (int32_t)n);
+    if (st != TRITD_OK) fail("tritd:devices", status_msg(st));
 }
 
 void do_triple_product(int, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
@@ -194,7 +225,13 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     char cmd[32] = {0};
     mxGetString(prhs[0], cmd, sizeof cmd);
     const std::string c(cmd);
-    if (c == "admm")
+    if (!g_at_exit_set) {
+        mexAtExit(at_exit);
+        g_at_exit_set = true;
+    }
+    if (c == "devices")
+        do_devices(nlhs, plhs, nrhs, prhs);
+    else if (c == "admm")
         do_admm(nlhs, plhs, nrhs, prhs);
     else if (c == "triple_product")
         do_triple_product(nlhs, plhs, nrhs, prhs);

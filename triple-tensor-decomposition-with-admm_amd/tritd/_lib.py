@@ -73,6 +73,8 @@ SIGNATURES = {
     "tritd_admm_sharded_virtual_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp,
                                                  vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32),
                                                  i32]),
+    "tritd_set_devices": (C.c_int, [C.POINTER(i32), i32]),
+    "tritd_shutdown": (None, []),
     "tritd_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp]),
     "tritd_unfold_f64": (C.c_int, [vp, i64, i64, i64, i32, vp]),
     "tritd_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp]),
@@ -107,6 +109,19 @@ def device_count():
     n = i32(0)
     check(lib.tritd_device_count(C.byref(n)))
     return n.value
+
+
+def set_devices(devices):
+    """Device set of triple_decomp_ADMM (tritd_set_devices): more than one
+    device shards D along mode 1 over them from this thread; one device
+    repeated runs virtual shards on it; [] clears the set."""
+    d = [int(x) for x in devices]
+    arr = (i32 * max(len(d), 1))(*d)
+    check(lib.tritd_set_devices(arr, len(d)))
+
+
+def shutdown():
+    lib.tritd_shutdown()
 
 
 _printer_ref = None
