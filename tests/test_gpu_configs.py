@@ -55,6 +55,28 @@ def test_rccl_single_rank_session(tritd):
                orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
 
 
+@pytest.mark.parametrize("name", ["g30_r3", "g12x10x8_r2_stop"])
+def test_sharded_schedule_matches_phase_order(tritd, name, monkeypatch):
+    """With a communicator the Grams of B, C and the solves of C, A(k+1) run
+    on a side stream (Session::iterate_sharded); same kernels on the same
+    inputs as the phase-serial order (TRITD_SHOV=0), so bitwise equal."""
+    g = load_golden(name)
+    n1, n2, n3 = g["D"].shape
+    out = []
+    for shov in ("1", "0"):
+        monkeypatch.setenv("TRITD_SHOV", shov)
+        comm = tritd.Comm(tritd.Comm.unique_id(), 1, 0, 0)
+        s = tritd.Session(g["r"], g["opts"], g["A0"], g["B0"], g["C0"], n1=n1, n2=n2, n3=n3,
+                          D=g["D"], device=0, comm=comm)
+        s.run(g["opts"]["maxIter"])
+        out.append(s.get())
+        s.close()
+        comm.close()
+    assert out[0]["k"] == out[1]["k"] == g["k"]
+    for key in ("A", "B", "C", "O", "E", "errHist"):
+        np.testing.assert_array_equal(out[0][key], out[1][key])
+
+
 def test_config2_sensor_shape_vs_c_oracle(tritd, cref):
     from tritd import synth
     mod, lib = cref

@@ -9,6 +9,9 @@
 //            M3(t,k) = sum_ij T(ij,t) A^(i,k) B^(j,k)   MFMA, this file's K2
 // F*F.' = (B^TB) o (C^TC) is the Hadamard identity of the Khatri-Rao design
 // matrices built by buildF/G/H (buildF.m:17-21): F, G, H are never formed.
+#include <algorithm>
+#include <string>
+#include <cstdlib>
 #include <utility>
 
 #include "kernels.h"
@@ -23,6 +26,9 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
 
 // ---------------------------------------------------------------------------
 // M1(i,k) = sum_j Wk[k][j*n1p + i] * Bh[j][k]; block = 64 rows x 4 j-slices
+// (A j-split over more workgroups for 64-row shards, joined by a last-arriver
+// ticket, cost more than it saved: the device-scope fences it needs write
+// back and invalidate L2 on gfx950 and slowed every following kernel.)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_m1(const double* __restrict__ Wk,
                                             const double* __restrict__ Bh, double* M1,
@@ -272,33 +278,55 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
 // ---------------------------------------------------------------------------
 // Gram: G[k][k'] = sum_i X[i][k] X[i][k'] (rows in 256/RP interleaved groups)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_gram(const double* __restrict__ X, int64_t rows, int RP,
-                                               double* G, const int* stop) {
+// G = X^T X (RP x RP) of a row-major rows x RP factor — the Hadamard-Gram
+// factors A^TA, B^TB, C^TC of update_A/B/C (:77,86,93 build F F^T etc.;
+// SURVEY.md §0.3).  One workgroup per 16 x 16 tile of G: the rows go to
+// v_mfma_f64_16x16x4_f64 four at a time (A[m][k] = X(i0+k, 16ta+m),
+// B[k][n] = X(i0+k, 16tb+n)), the 4 waves take every 4th K-step and are
+// summed through LDS in fixed order (deterministic).  Out-of-range rows load
+// as zero.  Latency-bound at these sizes; the old per-column VALU loop took
+// 29 us at 512 x 64, this takes a few.
+__global__ __launch_bounds__(256) void k_gram(const double* __restrict__ X, int64_t rows, int RP,
+                                              double* G, const int* stop) {
     if (stop && *stop) return;
-    const int k = blockIdx.x;
-    const int groups = 1024 / RP;
-    const int kk = threadIdx.x % RP, grp = threadIdx.x / RP;
-    double a0 = 0.0, a1 = 0.0;
-    const int64_t st = groups;
-    int64_t i = grp;
-    for (; i + st < rows; i += 2 * st) {
-        a0 = fma(X[i * RP + k], X[i * RP + kk], a0);
-        a1 = fma(X[(i + st) * RP + k], X[(i + st) * RP + kk], a1);
+    const int nt = RP >> 4;
+    const int ta = blockIdx.x / nt, tb = blockIdx.x - (blockIdx.x / nt) * nt;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m = lane & 15, kq = lane >> 4;
+    const double* xa = X + 16 * ta + m;
+    const double* xb = X + 16 * tb + m;
+    const int64_t steps = (rows + 3) >> 2;
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+    for (int64_t s = w; s < steps; s += 16) {  // K-steps s, s+4, s+8, s+12: loads first
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = 4 * (s + 4 * u) + kq;
+            const bool in = i < rows;
+            a[u] = in ? xa[i * RP] : 0.0;
+            b[u] = in ? xb[i * RP] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = mfma4(a[u], b[u], acc);
     }
-    if (i < rows) a0 = fma(X[i * RP + k], X[i * RP + kk], a0);
-    __shared__ double red[1024];
-    red[threadIdx.x] = a0 + a1;
+    __shared__ double part[3][4][64];
+    if (w > 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[w - 1][r][lane] = acc[r];
     __syncthreads();
-    if (grp == 0) {
-        double s = red[kk];
-        for (int q = 1; q < groups; ++q) s += red[q * RP + kk];
-        G[k * RP + kk] = s;
+    if (w == 0) {
+        // C/D element r of lane l: G(16ta + (l>>4) + 4r, 16tb + (l&15))
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double v = ((acc[r] + part[0][r][lane]) + part[1][r][lane]) + part[2][r][lane];
+            G[(int64_t)(16 * ta + kq + 4 * r) * RP + 16 * tb + m] = v;
+        }
     }
 }
 
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_gram, dim3(RP), dim3(1024), 0, st, X, rows, RP, G, stop);
+    hipLaunchKernelGGL(k_gram, dim3((RP / 16) * (RP / 16)), dim3(256), 0, st, X, rows, RP, G, stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -571,6 +599,186 @@ static size_t solve_big_lds(int RP) {
     return (size_t)(2 * SB * RP + SB * SB + 64 + RP) * sizeof(double);
 }
 
+// ---------------------------------------------------------------------------
+// Ginv = inv(P o Q + alpha I) at RP = 128 (fp32 path, r = 9..11): blocked
+// symmetric sweep with the matrix S in LDS (153 KB).  Per block K of 16
+// pivots (k0 = 16K):
+//   1. wave 0 sweeps the 16-row panel S_K,: pivot by pivot in registers
+//      (lane = column, pivot column by readlane) and records each pivot row
+//      at its pivot divided by the pivot, u_p = S_p,:/d_p; the pivots are the
+//      sequential sweep's (= LDL^T) pivots, kept for the pinv-tolerance check
+//   2. S_ij -= sum_p l_p[i] u_p[j] for i, j outside K (rank-16 f64 MFMA),
+//      with l_p[i] = u_p[i] d_p standing in for the column value S_ip, and
+//      S_iK = S_Kiᵀ
+// Accuracy (80-bit reference, 100-iteration solve of the sensor shape whose
+// Gram reaches cond ~1e6): the sequential sweep lands within 6e-11; this
+// form, whose column values come from the mirrored panel row, within
+// 3e-8..2e-7 — far below single precision, but not enough for the fp64
+// tolerance, so RP <= 64 uses the per-pivot sweep (k_solve).  (Forming D^-1
+// explicitly and multiplying, the textbook blocked form: 3e-5.)  Every
+// variant keeps RP sequential pivot steps of ~0.3 us (broadcast, IEEE
+// division, dependent update), so blocking pays only where the trailing
+// work dominates: 100 us vs 143 us for k_solve_big at RP = 128.
+// After all blocks S = -inv(.): Ginv = -S, identity pad zeroed.
+// ---------------------------------------------------------------------------
+template <int RP>
+constexpr int solve_blk_waves() { return RP >= 128 ? 8 : 4; }
+constexpr size_t solve_blk_lds(int RP) {
+    return ((size_t)RP * (RP + 4) + (size_t)16 * RP + RP) * sizeof(double);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const int2 b = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(b.x, l);
+    r.y = __builtin_amdgcn_readlane(b.y, l);
+    return __builtin_bit_cast(double, r);
+}
+
+template <int RP>
+__global__ __launch_bounds__(64 * solve_blk_waves<RP>()) void k_solve_blk(
+    const double* __restrict__ P, const double* __restrict__ Q, int R, double alpha, double* Ginv,
+    int* flags, const int* stop) {
+    if (*stop) return;
+    __builtin_amdgcn_s_setprio(3);  // beside K5 / M3 on the side stream: win issue
+    constexpr int LD = RP + 4, NB = RP / 16, NWV = solve_blk_waves<RP>(), NT = 64 * NWV;
+    constexpr int CPL = (RP + 63) / 64;  // panel columns per lane
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* S = sm;
+    double* Ub = sm + RP * LD;  // [16][RP]: u_p = S_p,: / d_p at pivot p
+    double* pivs = Ub + 16 * RP;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m = lane & 15, kq = lane >> 4;
+    {
+        constexpr int NE = (RP * RP + NT - 1) / NT;
+        double v[NE];
+#pragma unroll
+        for (int q = 0; q < NE; ++q) {  // loads first
+            const int e = tid + q * NT;
+            const int i = e / RP, c = e - (e / RP) * RP;
+            const bool in = e < RP * RP && i < R && c < R;
+            v[q] = in ? P[e] * Q[e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NE; ++q) {
+            const int e = tid + q * NT;
+            const int i = e / RP, c = e - (e / RP) * RP;
+            if (e < RP * RP) S[i * LD + c] = (i == c) ? ((i < R) ? v[q] + alpha : 1.0) : v[q];
+        }
+    }
+    __syncthreads();
+    for (int K = 0; K < NB; ++K) {
+        const int k0 = 16 * K;
+        if (w == 0) {
+            double pv[CPL][16];
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int c = lane + 64 * u;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) pv[u][r] = c < RP ? S[(k0 + r) * LD + c] : 0.0;
+            }
+            const int pl0 = k0 & 63, pu = k0 >> 6;  // lane / register set of pivot column k0
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                double colp[16];  // S_rp, r in K (current), from the lane owning column p
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    double x = pv[0][r];
+#pragma unroll
+                    for (int u = 1; u < CPL; ++u) x = (pu == u) ? pv[u][r] : x;
+                    colp[r] = readlane_f64(x, pl0 + q);
+                }
+                const double d = colp[q];
+                const double inv = 1.0 / d;
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) {
+                    const int c = lane + 64 * u;
+                    const bool cp = (c == k0 + q);
+                    const double sc = pv[u][q] * inv;  // a_pc / d
+                    if (c < RP) Ub[q * RP + c] = sc;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const double sw = pv[u][r] - colp[r] * sc;
+                        const double cq = colp[r] * inv;
+                        pv[u][r] = (r == q) ? (cp ? -inv : sc) : (cp ? cq : sw);
+                    }
+                }
+                if (lane == 0) pivs[k0 + q] = d;
+            }
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int c = lane + 64 * u;
+                if (c < RP)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) S[(k0 + r) * LD + c] = pv[u][r];
+            }
+        }
+        __syncthreads();
+        // trailing rank-16 update: A[m][kk] = -l_kk[16it + m], B[kk][n] = u_kk[16jt + n]
+        for (int t = w; t < NB * NB; t += NWV) {
+            const int it = t / NB, jt = t - (t / NB) * NB;
+            if (it == K || jt == K) continue;
+            d4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = S[(16 * it + kq + 4 * r) * LD + 16 * jt + m];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int kk = 4 * s4 + kq;
+                const double l = Ub[kk * RP + 16 * it + m] * pivs[k0 + kk];
+                acc = mfma4(-l, Ub[kk * RP + 16 * jt + m], acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[(16 * it + kq + 4 * r) * LD + 16 * jt + m] = acc[r];
+        }
+        for (int e = tid; e < 16 * RP; e += NT) {  // column block K (symmetry)
+            const int rr = e / RP, c = e - (e / RP) * RP;
+            if (c < k0 || c >= k0 + 16) S[c * LD + k0 + rr] = S[(k0 + rr) * LD + c];
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < RP * RP; e += NT) {
+        const int i = e / RP, j = e - (e / RP) * RP;
+        Ginv[e] = (i < R && j < R) ? -S[i * LD + j] : 0.0;
+    }
+    if (tid == 0) {
+        double minpiv = 1e308, maxpiv = 0.0;
+        for (int p = 0; p < R; ++p) {
+            minpiv = fmin(minpiv, pivs[p]);
+            maxpiv = fmax(maxpiv, pivs[p]);
+        }
+        const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);
+        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
+    }
+}
+
+template <int RP>
+void launch_solve_blk(int R, const double* P, const double* Q, double alpha, double* Ginv,
+                      int* flags, const int* stop, hipStream_t st) {
+    constexpr size_t lds = solve_blk_lds(RP);
+    static bool attr = false;
+    if (!attr && lds > 65536) {
+        TRITD_HIP(hipFuncSetAttribute((const void*)k_solve_blk<RP>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
+    attr = true;
+    hipLaunchKernelGGL(k_solve_blk<RP>, dim3(1), dim3(64 * solve_blk_waves<RP>()), lds, st, P, Q, R,
+                       alpha, Ginv, flags, stop);
+}
+
+// RP <= 64: per-pivot register sweep (k_solve); RP = 128: blocked sweep
+// (k_solve_blk); RP = 256: k_solve_big.  TRITD_SOLVE=blk runs the blocked
+// sweep at RP <= 64 too (timing / accuracy experiments), =sweep keeps
+// k_solve_big at 128.
+static int solve_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("TRITD_SOLVE");
+        if (!e) return 0;
+        const std::string x(e);
+        return x == "blk" ? 1 : (x == "sweep" ? 2 : 0);
+    }();
+    return v;
+}
+
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
                   int* flags, const int* stop, hipStream_t st) {
 #define SOLVE_CASE(RPV)                                                                      \
@@ -578,6 +786,18 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
         hipLaunchKernelGGL(k_solve<RPV>, dim3(1), dim3(RPV * 64 / SOLVE_ROWS), 0, st, P, Q, R, alpha, \
                            Ginv, flags, stop);                                               \
         break;
+    if ((RP == 128 && solve_mode() != 2) || (RP <= 64 && solve_mode() == 1)) {
+        switch (RP) {
+            case 16: launch_solve_blk<16>(R, P, Q, alpha, Ginv, flags, stop, st); break;
+            case 32: launch_solve_blk<32>(R, P, Q, alpha, Ginv, flags, stop, st); break;
+            case 48: launch_solve_blk<48>(R, P, Q, alpha, Ginv, flags, stop, st); break;
+            case 64: launch_solve_blk<64>(R, P, Q, alpha, Ginv, flags, stop, st); break;
+            case 128: launch_solve_blk<128>(R, P, Q, alpha, Ginv, flags, stop, st); break;
+            default: throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
+        }
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     switch (RP) {
         SOLVE_CASE(16)
         SOLVE_CASE(32)
@@ -606,39 +826,51 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
 // ---------------------------------------------------------------------------
 // Y = M * Ginv (rows x RP), optional transposed copy YT[k*ldT + i]
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_apply(const double* __restrict__ M, int64_t rows,
-                                               const double* __restrict__ Ginv, int RP, double* Y,
-                                               double* YT, int64_t ldT, const int* stop) {
+template <int RP>
+__global__ __launch_bounds__(64 * (RP / 16)) void k_apply(const double* __restrict__ M, int64_t rows,
+                                                           const double* __restrict__ Ginv, double* Y,
+                                                           double* YT, int64_t ldT, const int* stop) {
+    // one wave per 16 x 16 tile of Y: rows r0..r0+15, columns 16*tn..;
+    // v_mfma_f64_16x16x4_f64 over the RP/4 K-steps, every operand loaded
+    // before the chain (A[m][k] = M(r0+m, 4s+k), B[k][n] = Ginv(4s+k, 16tn+n))
     if (stop && *stop) return;
-    __shared__ double g[64 * 64];
-    __shared__ double m[16 * 65];
+    constexpr int KS = RP / 4;
+    const int lane = threadIdx.x & 63, tn = threadIdx.x >> 6;
+    const int m = lane & 15, kq = lane >> 4;
     const int64_t r0 = (int64_t)blockIdx.x * 16;
-    for (int e = threadIdx.x; e < RP * RP; e += 256) g[e] = Ginv[e];
-    for (int e = threadIdx.x; e < 16 * RP; e += 256) {
-        const int rr = e / RP, q = e - rr * RP;
-        m[rr * 65 + q] = (r0 + rr < rows) ? M[(r0 + rr) * RP + q] : 0.0;
+    const bool in = r0 + m < rows;
+    const double* mp = M + (r0 + m) * RP + kq;
+    const double* gp = Ginv + (int64_t)kq * RP + 16 * tn + m;
+    double a[KS], b[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        a[s] = in ? mp[4 * s] : 0.0;
+        b[s] = gp[(int64_t)4 * s * RP];
     }
-    __syncthreads();
-    const int rpb = 256 / RP;  // rows per pass
-    const int k = threadIdx.x % RP, rl = threadIdx.x / RP;
-    for (int rr = rl; rr < 16; rr += rpb) {
-        const int64_t i = r0 + rr;
-        if (i >= rows) break;
-        double s0 = 0.0, s1 = 0.0;
-        for (int q = 0; q < RP; q += 2) {
-            s0 = fma(m[rr * 65 + q], g[q * RP + k], s0);
-            s1 = fma(m[rr * 65 + q + 1], g[(q + 1) * RP + k], s1);
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = mfma4(a[s], b[s], acc);
+    // C/D element r of lane l: Y(r0 + (l>>4) + 4r, 16tn + (l&15))
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i = r0 + kq + 4 * r;
+        if (i < rows) {
+            Y[i * RP + 16 * tn + m] = acc[r];
+            if (YT) YT[(int64_t)(16 * tn + m) * ldT + i] = acc[r];
         }
-        const double s = s0 + s1;
-        Y[i * RP + k] = s;
-        if (YT) YT[(int64_t)k * ldT + i] = s;
     }
 }
 
 void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, double* Y, double* YT,
                   int64_t ldT, const int* stop, hipStream_t st) {
-    hipLaunchKernelGGL(k_apply, dim3((unsigned)cdiv(rows, 16)), dim3(256), 0, st, M, rows, Ginv,
-                       RP, Y, YT, ldT, stop);
+    const dim3 grid((unsigned)cdiv(rows, 16)), block(64 * (RP / 16));
+    switch (RP) {
+        case 16: hipLaunchKernelGGL(k_apply<16>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
+        case 32: hipLaunchKernelGGL(k_apply<32>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
+        case 48: hipLaunchKernelGGL(k_apply<48>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
+        case 64: hipLaunchKernelGGL(k_apply<64>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
+        default: throw Error(TRITD_ERR_UNSUPPORTED, "apply: RP not supported");
+    }
     TRITD_CHECK_LAUNCH();
 }
 

@@ -76,12 +76,6 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
                  hipStream_t shared_stream, bool defer_normD)
     : device_(device), o_(o), comm_(comm) {
     TRITD_HIP(hipSetDevice(device_));
-    if (shared_stream) {
-        st_ = shared_stream;
-    } else {
-        TRITD_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-        own_stream_ = true;
-    }
     g_ = make_geom(n1, n2, n3, i0, i1, r);
     f32_ = (flags & TRITD_SESSION_F32) != 0;
     es_ = f32_ ? sizeof(float) : sizeof(double);
@@ -93,9 +87,14 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         const char* rt = std::getenv("TRITD_ROT");
         rot_ = rt ? std::atoi(rt) : 0;
         if (ovmode_ == 0) overlap_ = false;
+        // one process per GPU with a communicator: the sharded schedule with
+        // its off-critical-path Grams and solves on the side stream
+        const char* sh = std::getenv("TRITD_SHOV");
+        shov_ = comm != nullptr && comm->comm != nullptr && shared_stream == nullptr &&
+                !(sh && std::atoi(sh) == 0);
     }
-    if (overlap_) {
-        TRITD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    create_streams(shared_stream);
+    if (overlap_ || shov_) {
         for (hipEvent_t* e : {&evAtA_, &evBtB_, &evCtC_, &evSA_, &evSB_, &evSC_})
             TRITD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
@@ -147,7 +146,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     ChT_.alloc((size_t)g_.RP * g_.n3p);
     M1_.alloc_bytes((size_t)g_.n1p * g_.RP * es_);
     Ginv_.alloc((size_t)g_.RP * g_.RP);
-    if (overlap_) {
+    if (overlap_ || shov_) {
         GinvA_.alloc((size_t)g_.RP * g_.RP);
         GinvB_.alloc((size_t)g_.RP * g_.RP);
         GinvC_.alloc((size_t)g_.RP * g_.RP);
@@ -208,7 +207,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
 
     // T of iteration 1 (:33) and W = T x3 C0 for update_A/update_B
     if (o_.maxIter > 0) launch_k5_any(1, /*prologue=*/true);
-    if (overlap_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
+    if (overlap_ || shov_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
         TRITD_HIP(hipEventRecord(evCtC_, st_));
         TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
         launch_solve(g_.RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
@@ -216,6 +215,28 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         TRITD_HIP(hipStreamSynchronize(side_));
     }
     TRITD_HIP(hipStreamSynchronize(st_));
+}
+
+// Streams.  The side stream (Grams and R x R solves beside K5 / M3) is
+// created at high priority: HIP maps streams of one priority onto a few
+// hardware queues, and a same-priority side stream was measured sharing the
+// main stream's queue (everything serialised, only the event waits added);
+// the high-priority pool is separate.  Side kernels still wait for free CU
+// slots while K5 / M3 occupy every SIMD; reserving CUs for them with
+// CU-masked streams (hipExtStreamCreateWithCUMask, 8 of 256 CUs) slowed K5
+// from 1.19 to 1.52 ms and M3 from 0.36 to 0.65 ms, so it is not used.
+void Session::create_streams(hipStream_t shared_stream) {
+    if (shared_stream) {
+        st_ = shared_stream;
+        return;
+    }
+    own_stream_ = true;
+    TRITD_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    if (overlap_ || shov_) {
+        int lo = 0, hi = 0;
+        TRITD_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        TRITD_HIP(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
+    }
 }
 
 Session::~Session() {
@@ -304,7 +325,7 @@ void Session::do_m3() {
         launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
 }
 
-// (X*F')*pinv(G): fp64 path through the LDS-staged apply (RP <= 64); fp32
+// (X*F')*pinv(G): fp64 path through the MFMA apply (RP <= 64); fp32
 // path single in, single-rounded out (MATLAB single * double = single)
 void Session::do_apply_A(const double* Ginv) {
     if (f32_)
@@ -526,6 +547,47 @@ void Session::iterate_overlapped(int k) {
     launch_k5_full(k, /*fused_finish=*/true);
 }
 
+// Sharded iteration (one process per GPU).  The all-reduce
+// of M2 + A^TA gates solve B, which stays on the critical path; the other two
+// solves and the two replicated Grams run on the side stream:
+//   main: M1 -> apply A -> Gram A -> M2 -> AR(M2, A^TA) -> solve B -> apply B
+//         -> M3 -> AR(M3) -> apply C -> K5 -> AR(norms) -> finish
+//   side: Gram B -> solve C (|| M3 + its AR) | Gram C -> solve A(k+1) (|| K5)
+// Hazards as in iterate_overlapped: every buffer a side kernel reads is next
+// written on the main stream only after an event recorded behind it.
+void Session::iterate_sharded(int k) {
+    const int RP = g_.RP;
+    double* M2 = red1_.p;
+    double* AtA = red1_.p + g_.n2 * RP;
+    do_m1();
+    TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
+    do_apply_A(GinvA_.p);
+    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    do_m2(M2);
+    allreduce(red1_.p, red1_count());
+    launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, GinvB_.p, ctrl_ + 2, ctrl_, st_);
+    do_apply_B(M2, GinvB_.p);
+    TRITD_HIP(hipEventRecord(evBtB_, st_));
+    TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, side_);  // :93 ridge
+    TRITD_HIP(hipEventRecord(evSC_, side_));
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    do_m3();
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+    allreduce(red2_.p, red2_count());
+    TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
+    do_apply_C(GinvC_.p);
+    TRITD_HIP(hipEventRecord(evCtC_, st_));
+    TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+    TRITD_HIP(hipEventRecord(evSA_, side_));
+    launch_k5_full(k, /*fused_finish=*/false);
+    allreduce(red3_.p, 2);
+    phaseD(k);
+}
+
 void Session::phaseD(int k) {
     launch_finish(red3_.p, normD_, k, o_.tol, errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_);
 }
@@ -561,6 +623,8 @@ void Session::run(int iters) {
         }
         if (overlap_) {
             iterate_overlapped(k);
+        } else if (shov_) {
+            iterate_sharded(k);
         } else {
             phaseA(k);
             allreduce(red1_.p, red1_count());

@@ -91,6 +91,11 @@ class Session {
     // single-GPU schedule: the three R x R solves run on a side stream, each
     // overlapped with the big kernel that precedes its consumer
     void iterate_overlapped(int k);
+    // one process per GPU with RCCL: the phase order with the Grams of B, C
+    // and the solves of C, A(k+1) on the side stream
+    void iterate_sharded(int k);
+    bool shov_ = false;
+    void create_streams(hipStream_t shared_stream);
     void launch_k5_full(int k, bool fused_finish);
     bool overlap_ = false;
     int ovmode_ = 2;
