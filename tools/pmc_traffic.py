@@ -5,7 +5,8 @@ Corrections (MI355X_MICROARCH.md §HBM): on gfx950 FETCH_SIZE reports half of
 the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE is
 exact for 16-B streaming stores.  Both counters are in KiB.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [algorithmic_bytes]
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [algorithmic_bytes [kernel]]
+(kernel: a substring of the kernel name, default k5_fused<64, false>)
 """
 import csv
 import glob
@@ -31,14 +32,15 @@ def per_dispatch(d, counter, kname="k5_fused<64, false>"):
 def main():
     fd, wd, out = sys.argv[1:4]
     alg = float(sys.argv[4]) if len(sys.argv) > 4 else None
-    fetch = per_dispatch(fd, "FETCH_SIZE")
-    write = per_dispatch(wd, "WRITE_SIZE")
+    kname = sys.argv[5] if len(sys.argv) > 5 else "k5_fused<64, false>"
+    fetch = per_dispatch(fd, "FETCH_SIZE", kname)
+    write = per_dispatch(wd, "WRITE_SIZE", kname)
     if not fetch or not write:
         raise SystemExit("no k5 dispatches found")
     med = lambda v: v[len(v) // 2]
     f_kib, w_kib = med(fetch), med(write)
     total = (2.0 * f_kib + w_kib) * 1024.0
-    res = {"kernel": "k5_fused<64,false>", "dispatches": [len(fetch), len(write)],
+    res = {"kernel": kname, "dispatches": [len(fetch), len(write)],
            "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
            "read_bytes_corrected": 2.0 * f_kib * 1024.0, "write_bytes": w_kib * 1024.0,
            "bytes_per_launch": total,

@@ -119,7 +119,7 @@ __device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
 // prefetch.
 __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, double* cs, double* CE,
                                           int64_t sb, d2v* E2, int64_t o,
-                                          unsigned long long* dense_tiles) {
+                                          unsigned& ndense) {
     uint64_t nz[4];
     int cnt = 0;
 #pragma unroll
@@ -155,7 +155,8 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
     if (dense) {
         E2[o] = d2v{En[0], En[1]};
         E2[o + 64] = d2v{En[2], En[3]};
-        if (lane == 0) atomicAdd(dense_tiles, 1ull);
+        ++ndense;  // wave-uniform; one atomic per wave at the end (a per-tile
+                   // atomic on one counter serialised: 17 -> 53 ms once E turned dense)
     }
     const __amdgpu_buffer_rsrc_t rs = wave_rsrc(CE + sb, CE_SLOT * 8);
     const double sv = (dense && l >= 4) ? 0.0 : v;
@@ -243,6 +244,7 @@ void k5_fused(K5Args a) {
     for (int m = 0; m < MT; ++m) wacc[m] = d4{0.0, 0.0, 0.0, 0.0};
 
     double ssL = 0.0, ssO = 0.0;
+    unsigned ndense = 0;  // E tiles of this wave stored densely (wave-uniform)
     const IterScalars sc = a.s;
     const d2v* D2 = reinterpret_cast<const d2v*>(a.D);
     d2v* O2 = reinterpret_cast<d2v*>(a.O);
@@ -365,7 +367,7 @@ void k5_fused(K5Args a) {
                 st2(YLn2, YL2 + o + 64 * p);
                 st2(YOn2, YO2 + o + 64 * p);
             }
-            ce_encode(En, lane, cs, a.CE, (tb >> 8) * CE_SLOT, E2, o, a.dense_tiles);
+            ce_encode(En, lane, cs, a.CE, (tb >> 8) * CE_SLOT, E2, o, ndense);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
         if (K5_EXP & 8) {
@@ -436,6 +438,9 @@ void k5_fused(K5Args a) {
                 a.Wk[(int64_t)(16 * m + tg + 4 * rr) * a.plane + wbase] = wacc[m][rr];
     }
 
+    if (!PRO && ndense && lane == 0)  // spread over DENSE_SLOTS counters
+        atomicAdd(a.dense_tiles + ((blockIdx.x * K5_WAVES + wid) & (DENSE_SLOTS - 1)),
+                  (unsigned long long)ndense);
     if (!PRO) {
         // fixed-order block reduction of the residual norms
 #pragma unroll

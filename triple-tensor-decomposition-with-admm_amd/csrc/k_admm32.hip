@@ -80,7 +80,7 @@ __device__ __forceinline__ bool ce32_decode(float sv, int lane, float (&e)[4]) {
 // LDS image (slot + junk area for the zeros: no divergent branch)
 __device__ __forceinline__ void ce32_encode(const float (&En)[4], int lane, float* cs,
                                             float* slot, f4* Etile,
-                                            unsigned long long* dense_tiles) {
+                                            unsigned& ndense) {
     uint64_t nz[4];
     int cnt = 0;
 #pragma unroll
@@ -111,7 +111,8 @@ __device__ __forceinline__ void ce32_encode(const float (&En)[4], int lane, floa
     const float v = cs[lane];
     if (dense) {
         Etile[lane] = f4{En[0], En[1], En[2], En[3]};
-        if (lane == 0) atomicAdd(dense_tiles, 1ull);
+        ++ndense;  // wave-uniform; one atomic per wave at the end (a per-tile
+                   // atomic on one counter serialised: 17 -> 53 ms once E turned dense)
     }
     slot[lane] = (dense && lane >= 8) ? 0.0f : v;
 }
@@ -198,6 +199,7 @@ void k5_f32(K5Args32 a) {
     for (int m = 0; m < MT; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 
     double ssL = 0.0, ssO = 0.0;
+    unsigned ndense = 0;  // E tiles of this wave stored densely (wave-uniform)
     const IterScalars32 sc = a.s;
     const f4* D4 = reinterpret_cast<const f4*>(a.D);
     f4* O4 = reinterpret_cast<f4*>(a.O);
@@ -294,7 +296,7 @@ void k5_f32(K5Args32 a) {
             YL4[o] = YLn;
             YO4[o] = YOn;
             if (K5F_EXP == 3) a.CE[(tb >> 8) * CE32_SLOT + lane] = En[0] + En[1] + En[2] + En[3];
-            else ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), a.dense_tiles);
+            else ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), ndense);
         }
         // T -> TX order through the wave's LDS tile: ts[t][ij]
 #pragma unroll
@@ -358,19 +360,37 @@ void k5_f32(K5Args32 a) {
     } else {
         body(tt, 0, xa, xb, false);
     }
-    if (active) {
-        // W^T C/D layout (f32): M-tile m row rho = 4(l>>4) + rr, col ij = l & 15;
-        // k = rho * MT + m (WB) or 16m + rho
-        const int64_t wbase = (tile << 4) + il;
+    {
+        // W out through LDS: a wave's 16 ij of a k-plane are 64 B, half an
+        // L2 line, and partial-line stores from four waves cost a line read +
+        // write each (K5 traffic 1.32x algorithmic at config 5).  The four
+        // waves hold four adjacent ij-tiles = 64 consecutive ij, so after the
+        // exchange every store is one 256 B row of a plane.  W^T C/D layout
+        // (f32): M-tile m row rho = 4(l>>4) + rr, col ij = l & 15;
+        // k = rho * MT + m (WB) or 16m + rho.
+        constexpr int WS = RP * 16 + 16;  // per-wave stride (pad: the read rows hit distinct banks)
+        __shared__ float wl[K5W * WS];
+        __syncthreads();  // sC / tsm reads of the last tile are done
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int rho = 4 * tg + rr;
                 const int k = WB ? rho * MT + m : 16 * m + rho;
-                a.Wk[(int64_t)k * a.plane + wbase] = wacc[m][rr];
+                wl[wid * WS + k * 16 + il] = wacc[m][rr];
             }
+        __syncthreads();
+        const int64_t t0 = (int64_t)blockIdx.x * K5W;      // first tile of the block
+        const int lw = lane >> 4;                           // source wave of this lane
+        const bool ok = t0 + lw < a.tiles;
+        float* dst = a.Wk + (t0 << 4) + lane;
+#pragma unroll 4
+        for (int k = wid; k < RP; k += K5W)
+            if (ok) dst[(int64_t)k * a.plane] = wl[lw * WS + k * 16 + il];
     }
+    if (!PRO && ndense && lane == 0)  // spread over DENSE_SLOTS counters
+        atomicAdd(a.dense_tiles + ((blockIdx.x * K5W + wid) & (DENSE_SLOTS - 1)),
+                  (unsigned long long)ndense);
     if (!PRO) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {

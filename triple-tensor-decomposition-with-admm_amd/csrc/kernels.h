@@ -8,6 +8,10 @@
 
 namespace tritd {
 
+// Dense-E tile statistics: one atomic per wave into one of DENSE_SLOTS
+// counters (summed on the host), not one per tile on a single counter.
+constexpr int DENSE_SLOTS = 64;
+
 struct DevState;  // solver.cpp
 
 // ---- K5: fused ADMM update (k_admm.hip) ----------------------------------
@@ -28,7 +32,7 @@ struct K5Args {
     int64_t n1p, n2, n3p, plane, tiles, ntt;
     IterScalars s;
     const int* stop;
-    unsigned long long* dense_tiles;  // running count of E tiles stored densely
+    unsigned long long* dense_tiles;  // DENSE_SLOTS running counts of E tiles stored densely
     int rot;  // rotate each workgroup's t-walk (0 = natural order)
 };
 int k5_grid(const Geom& g);

@@ -165,8 +165,9 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     errO_.alloc(mi);
     for (DBuf* b : {&errHist_, &errL_, &errO_, &red1_, &red2_, &red3_})
         TRITD_HIP(hipMemsetAsync(b->p, 0, b->n * sizeof(double), st_));
-    TRITD_HIP(hipMalloc(&ctrl_, 4 * sizeof(int) + sizeof(unsigned long long)));
-    TRITD_HIP(hipMemsetAsync(ctrl_, 0, 4 * sizeof(int) + sizeof(unsigned long long), st_));
+    const size_t ctrl_bytes = 4 * sizeof(int) + DENSE_SLOTS * sizeof(unsigned long long);
+    TRITD_HIP(hipMalloc(&ctrl_, ctrl_bytes));
+    TRITD_HIP(hipMemsetAsync(ctrl_, 0, ctrl_bytes, st_));
 
     // D -> tile-major device layout (one-off)
     if (g_.n1l > 0 && n2 * n3 > 0) {
@@ -441,6 +442,7 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     const size_t room = fr > reserve ? (fr - reserve) / pool_bytes : 0;
     if ((size_t)want > room) want = room > 1 ? (int)room : 1;
     std::vector<double*> cand;
+    // (hipDeviceMallocContiguous pools probe no differently: tools/contig_probe.py)
     for (int c = 0; c < want; ++c) {
         void* p = nullptr;
         if (hipMalloc(&p, pool_bytes) != hipSuccess) {
@@ -733,10 +735,12 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
 
 void Session::counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch) {
     TRITD_HIP(hipSetDevice(device_));
-    unsigned long long h = 0;
+    unsigned long long h[DENSE_SLOTS] = {};
     TRITD_HIP(hipStreamSynchronize(st_));
-    TRITD_HIP(hipMemcpy(&h, dense_tiles(), sizeof h, hipMemcpyDeviceToHost));
-    if (dense_tiles_total) *dense_tiles_total = (int64_t)h;
+    TRITD_HIP(hipMemcpy(h, dense_tiles(), sizeof h, hipMemcpyDeviceToHost));
+    unsigned long long t = 0;
+    for (unsigned long long x : h) t += x;
+    if (dense_tiles_total) *dense_tiles_total = (int64_t)t;
     if (tiles_per_launch) *tiles_per_launch = g_.Ntm / 256;
 }
 

@@ -139,7 +139,7 @@ class Session {
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;
     DBuf errHist_, errL_, errO_;
-    int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag, [4..5] u64 dense E tiles
+    int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag, then DENSE_SLOTS u64 dense-E counters
     unsigned long long* dense_tiles() const {
         return reinterpret_cast<unsigned long long*>(ctrl_ + 4);
     }
