@@ -198,6 +198,48 @@ tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t
                                             double* errHist, int32_t* iters, int32_t device);
 
 /* ---------------------------------------------------------------------------
+ * ALS variant: [A,B,C,errHist] = triple_decomp_ALS(X, r, opts)
+ * (fast_robust_triple_tensor/triple_decomp_ALS.m:1-40).
+ * Only opts.maxIter and opts.tol are read (:2-3): TRITD_OPT_MAXITER and
+ * TRITD_OPT_TOL must be present, a missing one fails like MATLAB.  errHist(k)
+ * = ||X - triple_product(A,B,C)||/||X|| is taken before the update of
+ * iteration k; the stop test (:20) returns the factors of that iteration
+ * un-updated, errHist = errHist(1:k).  Every mode uses the ridge 1e-9.  The
+ * progress line "Iteration %d, relative error = %.4e" goes to the print
+ * callback every 5 iterations (:17-19).  fp64, r <= 8.  device = -1 runs on
+ * the device set of tritd_set_devices (mode-1 shards).
+ * ------------------------------------------------------------------------- */
+tritd_status tritd_als_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                           const tritd_opts* opts, const double* A0, const double* B0,
+                           const double* C0, double* A, double* B, double* C, double* errHist,
+                           int32_t* iters, int32_t device);
+/* Steppable ALS session (bench, one process per GPU with comm; shard rows
+ * [i0, i1) as for tritd_session_create; flags: TRITD_SESSION_D_ON_DEVICE).
+ * quiet = 1 skips the every-5-iterations progress line (and its host
+ * synchronisation). */
+typedef struct tritd_als_session tritd_als_session;
+tritd_status tritd_als_session_create(tritd_als_session** out, int32_t device, const double* X,
+                                      int64_t ldX, int64_t n1, int64_t n2, int64_t n3, int64_t i0,
+                                      int64_t i1, int32_t r, const tritd_opts* opts,
+                                      const double* A0, const double* B0, const double* C0,
+                                      tritd_comm* comm, uint32_t flags, int32_t quiet);
+tritd_status tritd_als_session_run(tritd_als_session* s, int32_t iters);
+tritd_status tritd_als_session_sync(tritd_als_session* s, int32_t* iters_done, int32_t* stopped);
+tritd_status tritd_als_session_get(tritd_als_session* s, double* A, double* B, double* C,
+                                   double* errHist, int32_t* iters);
+/* timing: fit kernel (fused triple product + error + W) and mode-3 MTTKRP ms per launch */
+tritd_status tritd_als_session_set_timing(tritd_als_session* s, int32_t enable);
+tritd_status tritd_als_session_kernel_ms(tritd_als_session* s, double* fit_ms, double* mode3_ms,
+                                         double* iteration_ms, int32_t* samples);
+void tritd_als_session_destroy(tritd_als_session* s);
+/* Single-GPU rehearsal of the sharded ALS (virtual shards, as above). */
+tritd_status tritd_als_sharded_virtual_f64(const double* X, int64_t n1, int64_t n2, int64_t n3,
+                                           int32_t r, const tritd_opts* opts, const double* A0,
+                                           const double* B0, const double* C0, int32_t nshards,
+                                           double* A, double* B, double* C, double* errHist,
+                                           int32_t* iters, int32_t device);
+
+/* ---------------------------------------------------------------------------
  * Primitives (host pointers).  Each replaces the named reference file.
  * ------------------------------------------------------------------------- */
 /* triple_product.m:1-7: X = reshape(unfold(A,1)*buildF(B,C), n1,n2,n3). */

@@ -282,6 +282,50 @@ def triple_decomp_ADMM(D, r, opts, A0, B0, C0, trace_iters=(), printer=None):
     return A, B, C, O, errHist, E, k, trace
 
 
+def triple_decomp_ALS(X, r, opts, A0, B0, C0, printer=None):
+    """Restatement of fast_robust_triple_tensor/triple_decomp_ALS.m:1-40.
+
+    Returns ``(A, B, C, errHist, k)``; the reference returns the first four
+    (`:1`).  Only ``opts.maxIter`` and ``opts.tol`` are read (`:2-3`).  The
+    relative error is taken *before* the update of iteration k (`:15-16`), the
+    stop test leaves the factors of that iteration unchanged (`:20-23`), every
+    mode uses the hard-coded ridge 1e-9 (`:27,:32,:37`), and the progress line
+    is printed every 5 iterations unconditionally (`:17-19`).  ``unfold`` and
+    ``buildF/G/H`` resolve to the standalone files of
+    ``fast_robust_triple_tensor/`` (the same definitions as the ADMM's
+    locals); the ``reshape_*`` helpers are ALS-local copies (`:44-63`)
+    identical to the ADMM's.
+    """
+    for f in ("maxIter", "tol"):
+        if f not in opts:
+            raise KeyError(f"Reference to non-existent field '{f}'.")
+    maxIter = int(opts["maxIter"]); tol = float(opts["tol"])         # :2-3
+    X = as3(X)
+    n1, n2, n3 = X.shape                                             # :5
+    Xnorm = np.linalg.norm(X.ravel(order="F"))                       # :6
+    A = as3(A0).reshape((n1, r, r), order="F").copy(order="F")      # :8
+    B = as3(B0).reshape((r, n2, r), order="F").copy(order="F")      # :9
+    C = as3(C0).reshape((r, r, n3), order="F").copy(order="F")      # :10
+    errHist = np.zeros(max(maxIter, 0))                              # :12
+    ridge = 1e-9 * np.eye(r * r)
+    k = 0
+    for k in range(1, maxIter + 1):                                  # :14
+        Xhat = triple_product(A, B, C)                                # :15
+        errHist[k - 1] = np.linalg.norm(X.ravel(order="F") - Xhat.ravel(order="F")) / Xnorm  # :16
+        if k % 5 == 0:                                                # :17-19
+            (printer or print)("Iteration %d, relative error = %.4e" % (k, errHist[k - 1]))
+        if k > 1 and abs(errHist[k - 1] - errHist[k - 2]) < tol * errHist[k - 2]:  # :20
+            errHist = errHist[:k]                                     # :21
+            return A, B, C, errHist, k                                # :22
+        F = buildF(B, C)                                              # :25-28
+        A = reshape_A_from_A1((unfold(X, 1) @ F.T) @ pinv(F @ F.T + ridge), n1, r)
+        G = buildG(A, C)                                              # :30-33
+        B = reshape_B_from_B2((unfold(X, 2) @ G.T) @ pinv(G @ G.T + ridge), n2, r)
+        H = buildH(A, B)                                              # :35-38
+        C = reshape_C_from_C3((unfold(X, 3) @ H.T) @ pinv(H @ H.T + ridge), n3, r)
+    return A, B, C, errHist, k
+
+
 def mu_schedule(mu0, rho, n):
     """The deterministic penalty sequence of :16 and :56 (muL == muO always)."""
     out = []

@@ -20,8 +20,10 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
-def golden_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+def golden_names(kind="admm"):
+    """Committed golden cases: triple_decomp_ADMM (g*.npz) or triple_decomp_ALS (als*.npz)."""
+    pat = {"admm": "g*.npz", "als": "als*.npz"}[kind]
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, pat)))
 
 
 def load_golden(name):
@@ -47,3 +49,9 @@ def gpu_available():
         return tritd.device_count() > 0
     except Exception:
         return False
+
+
+@pytest.fixture(scope="session")
+def synth():
+    from tritd import synth as s
+    return s

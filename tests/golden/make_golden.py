@@ -46,6 +46,31 @@ CASES = {
 }
 
 
+# triple_decomp_ALS.m: reads only maxIter and tol
+ALS_CASES = {
+    "als12x10x8_r2": (synth.low_rank_plus_outliers, dict(n1=12, n2=10, n3=8, r=2), 2,
+                      dict(maxIter=40, tol=1e-5)),
+    "als30_r3": (synth.low_rank_plus_outliers, dict(n1=30, n2=30, n3=30, r=3), 3,
+                 dict(maxIter=60, tol=1e-5)),
+    "als17x16x20_r8": (synth.low_rank_plus_outliers, dict(n1=17, n2=16, n3=20, r=8), 8,
+                       dict(maxIter=25, tol=1e-5)),
+    # early stop (:20-23): the factors of the stopping iteration are returned un-updated
+    "als20x24x18_r5_stop": (synth.video_like, dict(n1=20, n2=24, n3=18, r=5), 5,
+                            dict(maxIter=50, tol=1e-2)),
+}
+
+
+def make_als(name):
+    gen, kw, r, opts = ALS_CASES[name]
+    d = gen(**kw)
+    A, B, C, eh, k = orc.triple_decomp_ALS(d["D"], r, opts, d["A0"], d["B0"], d["C0"],
+                                           printer=lambda s: None)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), X=d["D"], A0=d["A0"], B0=d["B0"],
+                        C0=d["C0"], r=np.int64(r), opts=np.array(json.dumps(opts)), A=A, B=B,
+                        C=C, errHist=eh, k=np.int64(k))
+    return k, eh[-1]
+
+
 def make(name):
     gen, kw, r, opts, full = CASES[name]
     d = gen(**kw)
@@ -67,5 +92,11 @@ def make(name):
 
 
 if __name__ == "__main__":
-    for n in CASES:
-        print(n, *make(n))
+    # python tests/golden/make_golden.py [admm|als]  (default: both)
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "admm"):
+        for n in CASES:
+            print(n, *make(n))
+    if which in ("all", "als"):
+        for n in ALS_CASES:
+            print(n, *make_als(n))

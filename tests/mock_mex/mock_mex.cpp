@@ -189,4 +189,54 @@ int mock_admm(const void* D, long n1, long n2, long n3, int r, const char* opt_n
         if (a) mxDestroyArray(a);
     return rc;
 }
+
+// [A,B,C,errHist] = tritd_mex('als', X, r, opts, A0, B0, C0)
+int mock_als(const double* X, long n1, long n2, long n3, int r, const char* opt_names,
+             const double* opt_vals, const double* A0, const double* B0, const double* C0,
+             double* A, double* B, double* C, double* errHist, int* k, char* err, int errlen,
+             char* printed, int printlen) {
+    std::vector<mxArray*> in;
+    in.push_back(cmd_arg("als"));
+    in.push_back(dbl(X, {(mwSize)n1, (mwSize)n2, (mwSize)n3}));
+    double rr = r;
+    in.push_back(dbl(&rr, {1, 1}));
+    auto* opts = new mxArray;
+    opts->cls = mxSTRUCT_CLASS;
+    opts->dims = {1, 1};
+    {
+        std::string names(opt_names);
+        size_t pos = 0;
+        int q = 0;
+        while (pos <= names.size() && !names.empty()) {
+            const size_t c = names.find(',', pos);
+            const std::string nm = names.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+            opts->fields[nm] = dbl(&opt_vals[q++], {1, 1});
+            if (c == std::string::npos) break;
+            pos = c + 1;
+        }
+    }
+    in.push_back(opts);
+    in.push_back(dbl(A0, {(mwSize)n1, (mwSize)r, (mwSize)r}));
+    in.push_back(dbl(B0, {(mwSize)r, (mwSize)n2, (mwSize)r}));
+    in.push_back(dbl(C0, {(mwSize)r, (mwSize)r, (mwSize)n3}));
+    mxArray* out[4] = {nullptr};
+    int rc = 0;
+    g_printed.clear();
+    try {
+        mexFunction(4, out, (int)in.size(), const_cast<const mxArray**>(in.data()));
+        std::memcpy(A, out[0]->data.data(), (size_t)n1 * r * r * 8);
+        std::memcpy(B, out[1]->data.data(), (size_t)r * n2 * r * 8);
+        std::memcpy(C, out[2]->data.data(), (size_t)r * r * n3 * 8);
+        *k = (int)out[3]->dims[0];
+        std::memcpy(errHist, out[3]->data.data(), (size_t)*k * 8);
+    } catch (const MockMexError& e) {
+        std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
+        rc = 1;
+    }
+    std::snprintf(printed, printlen, "%s", g_printed.c_str());
+    for (auto* a : in) mxDestroyArray(a);
+    for (auto* a : out)
+        if (a) mxDestroyArray(a);
+    return rc;
+}
 }

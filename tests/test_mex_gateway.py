@@ -24,6 +24,7 @@ def gw(tmp_path_factory):
                     "-L" + libdir, "-ltritd", "-Wl,-rpath," + libdir, "-o", str(out)], check=True)
     lib = C.CDLL(str(out))
     lib.mock_admm.restype = C.c_int
+    lib.mock_als.restype = C.c_int
     return lib
 
 
@@ -129,3 +130,52 @@ def test_gateway_single_class_and_device_set(gw):
         np.testing.assert_allclose(two["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
     finally:
         assert devices(gw, [])[0] == 0
+
+
+# ---------------------------------------------------------------------------
+# 'als' command (matlab/triple_decomp_ALS.m -> tritd_als_f64)
+# ---------------------------------------------------------------------------
+def run_als(gw, g, names=("maxIter", "tol"), vals=None):
+    X = np.asfortranarray(g["X"])
+    n1, n2, n3 = X.shape
+    r = g["r"]
+    names = list(names)
+    vals = np.array(vals if vals is not None else [float(g["opts"][n]) for n in names])
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cc = np.zeros((r, r, n3), order="F")
+    eh = np.zeros(int(g["opts"]["maxIter"]) + 1)
+    k = C.c_int(0)
+    err = C.create_string_buffer(1024)
+    pr = C.create_string_buffer(4096)
+    p = lambda a: C.c_void_p(a.ctypes.data)
+    A0, B0, C0 = (np.asfortranarray(g[x]) for x in ("A0", "B0", "C0"))
+    rc = gw.mock_als(p(X), n1, n2, n3, r, ",".join(names).encode(), p(vals), p(A0), p(B0), p(C0),
+                     p(A), p(B), p(Cc), p(eh), C.byref(k), err, 1024, pr, 4096)
+    return rc, err.value.decode(), dict(A=A, B=B, C=Cc, errHist=eh[: k.value], k=k.value,
+                                        printed=pr.value.decode())
+
+
+def test_gateway_als_missing_field_error(gw):
+    g = load_golden("als12x10x8_r2")
+    rc, err, _ = run_als(gw, g, names=("tol", "mu"), vals=[1e-5, 1.0])
+    assert rc == 1
+    assert err == "MATLAB:nonExistentField|Reference to non-existent field 'maxIter'."
+    rc, err, _ = run_als(gw, g, names=("maxIter",), vals=[5.0])
+    assert err == "MATLAB:nonExistentField|Reference to non-existent field 'tol'."
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["als30_r3", "als20x24x18_r5_stop"])
+def test_gateway_als_matches_golden(gw, name):
+    import tritd_oracle as orc
+    g = load_golden(name)
+    rc, err, res = run_als(gw, g)
+    assert rc == 0, err
+    assert res["k"] == g["k"]
+    assert rel(orc.triple_product(res["A"], res["B"], res["C"]),
+               orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
+    np.testing.assert_allclose(res["errHist"], g["errHist"], rtol=1e-9, atol=1e-14)
+    lines = res["printed"].splitlines()
+    assert lines == ["Iteration %d, relative error = %.4e" % (i, g["errHist"][i - 1])
+                     for i in range(5, g["k"] + 1, 5)]

@@ -20,12 +20,6 @@ from conftest import golden_names, load_golden, rel
 import tritd_oracle as orc
 
 
-@pytest.fixture(scope="module")
-def synth():
-    from tritd import synth as s
-    return s
-
-
 @pytest.mark.parametrize("dims", [(5, 4, 3, 2), (3, 6, 4, 3), (4, 3, 5, 1)])
 def test_design_matrices_match_loop_definitions(synth, dims):
     n1, n2, n3, r = dims
@@ -169,3 +163,73 @@ def test_c_restatement_primitives(cref, synth):
         out = np.zeros(orc.unfold(X, mode).shape, order="F")
         lib.tritd_ref_unfold(p(X), 7, 5, 6, mode, p(out))
         np.testing.assert_array_equal(out, orc.unfold(X, mode))
+
+
+# ---------------------------------------------------------------------------
+# triple_decomp_ALS (fast_robust_triple_tensor/triple_decomp_ALS.m)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", golden_names("als"))
+def test_oracle_als_reproduces_golden(name):
+    g = load_golden(name)
+    A, B, C, eh, k = orc.triple_decomp_ALS(g["X"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                           printer=lambda s: None)
+    assert k == g["k"] and len(eh) == k
+    for key, X in (("A", A), ("B", B), ("C", C)):
+        assert rel(X, g[key]) <= 1e-12, key
+    np.testing.assert_allclose(eh, g["errHist"], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", golden_names("als"))
+def test_als_golden_stop_semantics(name):
+    """:20-23: the stop test fires on the first k > 1 whose relative change is
+    below tol, errHist is truncated to k; otherwise all maxIter entries."""
+    g = load_golden(name)
+    e, tol, k = g["errHist"], g["opts"]["tol"], g["k"]
+    rel_change = np.abs(np.diff(e)) / e[:-1]
+    fired = np.nonzero(rel_change < tol)[0]
+    if k < g["opts"]["maxIter"]:
+        assert len(fired) == 1 and fired[0] == k - 2
+    else:
+        assert len(fired) == 0 and k == g["opts"]["maxIter"]
+
+
+def test_als_error_is_taken_before_the_update():
+    """errHist(k) is the fit of the factors entering iteration k (:15-16), and
+    a stop at k returns those factors un-updated (:22)."""
+    g = load_golden("als20x24x18_r5_stop")
+    k = g["k"]
+    Xhat = orc.triple_product(g["A"], g["B"], g["C"])
+    e_k = np.linalg.norm((g["X"] - Xhat).ravel()) / np.linalg.norm(g["X"].ravel())
+    assert abs(e_k - g["errHist"][k - 1]) <= 1e-13 * e_k
+    # one iteration: errHist(1) is the fit of the initial factors
+    _, _, _, eh1, k1 = orc.triple_decomp_ALS(g["X"], g["r"], dict(maxIter=1, tol=1e-5), g["A0"],
+                                             g["B0"], g["C0"], printer=lambda s: None)
+    Xhat0 = orc.triple_product(g["A0"], g["B0"], g["C0"])
+    assert k1 == 1
+    assert abs(eh1[0] - np.linalg.norm((g["X"] - Xhat0).ravel()) / np.linalg.norm(g["X"].ravel())) < 1e-14
+
+
+def test_als_recovers_exact_low_rank(synth):
+    """Known answer: on an exactly rank-r^2 tensor (no outliers) ALS drives the
+    relative error down by orders of magnitude, and the error never rises by
+    more than rounding (each update is a ridge-1e-9 least-squares solve)."""
+    A, B, C = synth.random_factors(14, 12, 10, 2, seed=3)
+    X = orc.triple_product(A, B, C)
+    A0, B0, C0 = synth.random_factors(14, 12, 10, 2, seed=4)
+    _, _, _, eh, k = orc.triple_decomp_ALS(X, 2, dict(maxIter=200, tol=1e-12), A0, B0, C0,
+                                           printer=lambda s: None)
+    assert eh[-1] < 1e-9 * eh[0]
+    assert np.all(np.diff(eh) <= 1e-9 * eh[:-1] + 1e-13)  # rounding floor ~1e-10
+
+
+def test_als_opts_and_print():
+    g = load_golden("als12x10x8_r2")
+    with pytest.raises(KeyError, match="maxIter"):
+        orc.triple_decomp_ALS(g["X"], 2, dict(tol=1e-5), g["A0"], g["B0"], g["C0"])
+    with pytest.raises(KeyError, match="tol"):
+        orc.triple_decomp_ALS(g["X"], 2, dict(maxIter=3), g["A0"], g["B0"], g["C0"])
+    lines = []
+    _, _, _, eh, k = orc.triple_decomp_ALS(g["X"], 2, dict(maxIter=12, tol=0.0, mu=1), g["A0"],
+                                           g["B0"], g["C0"], printer=lines.append)
+    assert k == 12
+    assert lines == ["Iteration %d, relative error = %.4e" % (i, eh[i - 1]) for i in (5, 10)]

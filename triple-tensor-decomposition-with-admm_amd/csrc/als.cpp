@@ -1,0 +1,288 @@
+// Device-resident ALS loop of fast_robust_triple_tensor/triple_decomp_ALS.m:1-40.
+//
+// Iteration k (reference order):
+//   fit    Xhat = triple_product(A,B,C), errHist(k) = ||X - Xhat||/Xnorm   :15-16
+//          + W = X x3 C^ for the next two updates (k_als.hip)
+//   print  every 5 iterations                                               :17-19
+//   stop   k > 1 && |e_k - e_{k-1}| < tol e_{k-1}: truncate, return         :20-23
+//          (device flag: the update kernels of k early-exit)
+//   A      M1 = X1 F' from W, solve (B^TB o C^TC + 1e-9 I), apply          :25-28
+//   B      M2 = X2 G' from W and the new A, solve (A^TA o C^TC + 1e-9 I)    :30-33
+//   C      M3 = X3 H' (K2 over the TX copy of X), solve (A^TA o B^TB + 1e-9 I) :35-38
+// Sharded along mode 1 like the ADMM: the fit sum, [M2 | A^TA]
+// and M3 are the three reductions.
+#include "als.h"
+
+#include <cmath>
+#include <cstdlib>
+
+namespace tritd {
+
+void emit_line(const char* line);  // api.cpp
+
+AlsSession::AlsSession(int device, const double* X, int64_t ldX, int64_t n1, int64_t n2,
+                       int64_t n3, int64_t i0, int64_t i1, int r, int maxIter, double tol,
+                       const double* A0, const double* B0, const double* C0, tritd_comm* comm,
+                       uint32_t flags, hipStream_t shared_stream, bool defer_norm)
+    : device_(device), maxIter_(maxIter < 0 ? 0 : maxIter), tol_(tol), comm_(comm) {
+    TRITD_HIP(hipSetDevice(device_));
+    g_ = make_geom(n1, n2, n3, i0, i1, r);
+    if (!rp_supported(g_.RP))
+        throw Error(TRITD_ERR_UNSUPPORTED, "r must be in 1..8 for the fp64 ALS path");
+    if (shared_stream) {
+        st_ = shared_stream;
+    } else {
+        own_stream_ = true;
+        TRITD_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    }
+    const size_t Np = (size_t)g_.Ntm;
+    X_.alloc(Np);
+    XT_.alloc(Np);
+    TRITD_HIP(hipMemsetAsync(X_.p, 0, Np * sizeof(double), st_));
+    Wk_.alloc((size_t)g_.RP * g_.plane);
+    TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.bytes(), st_));
+    Ah_.alloc(g_.n1p * g_.RP);
+    AhT_.alloc((size_t)g_.RP * g_.n1p);
+    Bh_.alloc(g_.n2 * g_.RP);
+    Ch_.alloc(g_.n3p * g_.RP);
+    ChT_.alloc((size_t)g_.RP * g_.n3p);
+    M1_.alloc(g_.n1p * g_.RP);
+    Ginv_.alloc((size_t)g_.RP * g_.RP);
+    BtB_.alloc((size_t)g_.RP * g_.RP);
+    CtC_.alloc((size_t)g_.RP * g_.RP);
+    red0_.alloc(2);
+    red1_.alloc(red1_count());
+    red2_.alloc(red2_count());
+    fitpart_.alloc(2 * (size_t)als_fit_grid(g_));
+    m3part_.alloc((size_t)m3_parts(g_) * g_.n3p * g_.RP);
+    sqpart_.alloc(2 * (size_t)sumsq_blocks(g_));
+    errHist_.alloc(maxIter_ > 0 ? (size_t)maxIter_ : 1);
+    for (DBuf* b : {&errHist_, &red0_, &red1_, &red2_})
+        TRITD_HIP(hipMemsetAsync(b->p, 0, b->n * sizeof(double), st_));
+    TRITD_HIP(hipMalloc(&ctrl_, 4 * sizeof(int)));
+    TRITD_HIP(hipMemsetAsync(ctrl_, 0, 4 * sizeof(int), st_));
+
+    // X -> tile-major, and its TX copy for the mode-3 contraction (one-off)
+    if (g_.n1l > 0) {
+        if (flags & TRITD_SESSION_D_ON_DEVICE) {
+            launch_to_tm(g_, X, ldX, X_.p, st_);
+        } else {
+            DBuf tmp;
+            tmp.alloc((size_t)(g_.n1l * n2 * n3));
+            TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * sizeof(double), X, ldX * sizeof(double),
+                                       g_.n1l * sizeof(double), (size_t)(n2 * n3),
+                                       hipMemcpyHostToDevice, st_));
+            launch_to_tm(g_, tmp.p, g_.n1l, X_.p, st_);
+            TRITD_HIP(hipStreamSynchronize(st_));
+        }
+    }
+    launch_tm_to_tx(g_, X_.p, XT_.p, st_);
+
+    std::vector<double> Ah, AhT, Bh, Ch, ChT;
+    pack_A(g_, A0, Ah, AhT);
+    pack_B(g_, B0, Bh);
+    pack_C(g_, C0, Ch, ChT);
+    TRITD_HIP(hipMemcpy(Ah_.p, Ah.data(), Ah.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(AhT_.p, AhT.data(), AhT.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(Bh_.p, Bh.data(), Bh.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(Ch_.p, Ch.data(), Ch.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRITD_HIP(hipMemcpy(ChT_.p, ChT.data(), ChT.size() * sizeof(double), hipMemcpyHostToDevice));
+
+    // Xnorm = norm(X(:))  (:6)
+    const int nb = sumsq_blocks(g_);
+    launch_sumsq_padded(g_, X_.p, sqpart_.p, nb, st_);
+    launch_reduce_pairs(sqpart_.p, nb, red0_.p, nullptr, st_);
+    if (!defer_norm) {
+        allreduce(red0_.p, 2);
+        set_norm_from_red0();
+    }
+    // Grams of the initial B, C (replicated)
+    launch_gram(g_.RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    launch_gram(g_.RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    TRITD_HIP(hipStreamSynchronize(st_));
+}
+
+AlsSession::~AlsSession() {
+    (void)hipSetDevice(device_);
+    if (st_) (void)hipStreamSynchronize(st_);
+    for (auto e : ev_) (void)hipEventDestroy(e);
+    if (ctrl_) (void)hipFree(ctrl_);
+    if (own_stream_ && st_) (void)hipStreamDestroy(st_);
+}
+
+void AlsSession::set_norm_from_red0() {
+    double ss[2];
+    TRITD_HIP(hipMemcpyAsync(ss, red0_.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    Xnorm_ = std::sqrt(ss[0]);
+}
+
+void AlsSession::allreduce(double* buf, int64_t count) {
+    if (!comm_ || !comm_->comm) return;
+    const ncclResult_t r =
+        ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, comm_->comm, st_);
+    if (r != ncclSuccess)
+        throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+int AlsSession::next_iter() {
+    if (k_enq_ >= maxIter_) return 0;
+    return ++k_enq_;
+}
+
+void AlsSession::phaseFit(int k) {
+    (void)k;
+    AlsFitArgs a{};
+    a.X = X_.p; a.Wk = Wk_.p; a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p;
+    a.partial = fitpart_.p;
+    a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
+    a.ntt = g_.ntt;
+    a.stop = ctrl_;
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    launch_als_fit(g_, a, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+    launch_reduce_pairs(fitpart_.p, als_fit_grid(g_), red0_.p, ctrl_, st_);
+}
+
+void AlsSession::phaseErr(int k) {
+    launch_als_finish(red0_.p, Xnorm_, k, tol_, errHist_.p, ctrl_, st_);
+}
+
+void AlsSession::phaseA(int k) {
+    (void)k;
+    const int RP = g_.RP;
+    double* M2 = red1_.p;
+    double* AtA = red1_.p + g_.n2 * RP;
+    launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    launch_solve(RP, g_.R, BtB_.p, CtC_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :27
+    launch_apply(RP, M1_.p, g_.n1p, Ginv_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
+}
+
+void AlsSession::phaseB(int k) {
+    (void)k;
+    const int RP = g_.RP;
+    const double* M2 = red1_.p;
+    const double* AtA = red1_.p + g_.n2 * RP;
+    launch_solve(RP, g_.R, AtA, CtC_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :32
+    launch_apply(RP, M2, g_.n2, Ginv_.p, Bh_.p, nullptr, 0, ctrl_, st_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
+    launch_m3(g_, XT_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 2], st_));
+}
+
+void AlsSession::phaseC(int k) {
+    (void)k;
+    const int RP = g_.RP;
+    const double* AtA = red1_.p + g_.n2 * RP;
+    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :37
+    launch_apply(RP, red2_.p, g_.n3p, Ginv_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+}
+
+void AlsSession::maybe_print(int k) {
+    if (quiet_ || k % 5 != 0) return;  // :17
+    if (comm_ && comm_->rank != 0) return;
+    int ctrl[2];
+    double e;
+    TRITD_HIP(hipMemcpyAsync(ctrl, ctrl_, 2 * sizeof(int), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipMemcpyAsync(&e, errHist_.p + (k - 1), sizeof(double), hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    if (ctrl[1] != k) return;  // the loop broke before iteration k
+    char line[128];
+    std::snprintf(line, sizeof line, "Iteration %d, relative error = %.4e", k, e);  // :18
+    emit_line(line);
+}
+
+void AlsSession::run(int iters) {
+    TRITD_HIP(hipSetDevice(device_));
+    for (int it = 0; it < iters; ++it) {
+        const int k = next_iter();
+        if (!k) break;
+        if (timing_) {
+            for (int e = 0; e < 5; ++e) {
+                hipEvent_t ev;
+                TRITD_HIP(hipEventCreate(&ev));
+                ev_.push_back(ev);
+            }
+        }
+        phaseFit(k);
+        allreduce(red0_.p, 2);
+        phaseErr(k);
+        maybe_print(k);
+        phaseA(k);
+        allreduce(red1_.p, red1_count());
+        phaseB(k);
+        allreduce(red2_.p, red2_count());
+        phaseC(k);
+        if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 1], st_));
+    }
+}
+
+void AlsSession::harvest_timing() {
+    // events per iteration: [0] fit start, [1] fit end, [2] M3 start, [3] M3 end, [4] end
+    for (size_t b = 0; b + 5 <= ev_.size(); b += 5) {
+        float it = 0, m3 = 0, fit = 0;
+        TRITD_HIP(hipEventElapsedTime(&it, ev_[b], ev_[b + 4]));
+        TRITD_HIP(hipEventElapsedTime(&fit, ev_[b], ev_[b + 1]));
+        TRITD_HIP(hipEventElapsedTime(&m3, ev_[b + 2], ev_[b + 3]));
+        acc_it_ += it;
+        acc_fit_ += fit;
+        acc_m3_ += m3;
+        ++acc_n_;
+    }
+    for (auto e : ev_) (void)hipEventDestroy(e);
+    ev_.clear();
+}
+
+void AlsSession::set_timing(bool on) {
+    timing_ = on;
+    acc_fit_ = acc_m3_ = acc_it_ = 0;
+    acc_n_ = 0;
+}
+
+void AlsSession::kernel_ms(double* fit, double* m3, double* it, int* samples) {
+    const double n = acc_n_ ? (double)acc_n_ : 1.0;
+    if (fit) *fit = acc_fit_ / n;
+    if (m3) *m3 = acc_m3_ / n;
+    if (it) *it = acc_it_ / n;
+    if (samples) *samples = acc_n_;
+}
+
+void AlsSession::sync(int* done, int* stopped) {
+    TRITD_HIP(hipSetDevice(device_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    if (!ev_.empty()) harvest_timing();
+    int ctrl[2];
+    TRITD_HIP(hipMemcpy(ctrl, ctrl_, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    if (done) *done = ctrl[1];
+    if (stopped) *stopped = ctrl[0];
+}
+
+void AlsSession::get(double* A, double* B, double* C, double* errHist, int* iters) {
+    int done = 0, stopped = 0;
+    sync(&done, &stopped);
+    if (A) {
+        std::vector<double> h(Ah_.n);
+        TRITD_HIP(hipMemcpy(h.data(), Ah_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        unpack_A(g_, h, A);
+    }
+    if (B) {
+        std::vector<double> h(Bh_.n);
+        TRITD_HIP(hipMemcpy(h.data(), Bh_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        unpack_B(g_, h, B);
+    }
+    if (C) {
+        std::vector<double> h(Ch_.n);
+        TRITD_HIP(hipMemcpy(h.data(), Ch_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        unpack_C(g_, h, C);
+    }
+    if (errHist && done > 0)
+        TRITD_HIP(hipMemcpy(errHist, errHist_.p, (size_t)done * sizeof(double),
+                            hipMemcpyDeviceToHost));
+    if (iters) *iters = done;
+}
+
+}  // namespace tritd

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "als.h"
 #include "solver.h"
 
 using namespace tritd;
@@ -50,6 +51,15 @@ void check_opts(const tritd_opts* o) {
     for (const auto& f : fields)
         if (!(o->present & f.bit))
             throw Error(TRITD_ERR_OPTS, std::string("Reference to non-existent field '") + f.name + "'.");
+}
+
+// triple_decomp_ALS.m:2-3 reads only these two, in this order
+void check_als_opts(const tritd_opts* o) {
+    if (!o) throw Error(TRITD_ERR_OPTS, "opts is NULL");
+    if (!(o->present & TRITD_OPT_MAXITER))
+        throw Error(TRITD_ERR_OPTS, "Reference to non-existent field 'maxIter'.");
+    if (!(o->present & TRITD_OPT_TOL))
+        throw Error(TRITD_ERR_OPTS, "Reference to non-existent field 'tol'.");
 }
 
 tritd_opts normalized(const tritd_opts* o) {
@@ -113,88 +123,111 @@ void group_comms(const std::vector<int>& devs) {
     g_comm_devs = devs;
 }
 
-// One problem sharded along mode 1 over `devs`, driven from
-// the calling thread (§8b Threading): every iteration runs the four phases of
-// solver.cpp on each shard, and the three reductions between them are one
-// grouped ncclAllReduce per buffer over the shards' streams (distinct
-// devices), or an in-device sum of the shards' buffers when one device is
-// repeated (virtual shards: the sharded schedule on one GPU).  D, O, E are
-// column-major n1 x n2 x n3 host arrays of es-byte elements.
-void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t flags, int64_t n1,
-               int64_t n2, int64_t n3, int32_t r, const tritd_opts& o, const double* A0,
-               const double* B0, const double* C0, double* A, double* B, double* C, void* O,
-               void* E, double* errHist, int32_t* iters) {
-    const int P = (int)devs.size();
-    if (P < 1 || P > 16) throw Error(TRITD_ERR_ARG, "a device set holds 1..16 devices");
-    if (P > n1) throw Error(TRITD_ERR_ARG, "more shards than mode-1 rows");
-    bool same = true, distinct = true;
-    for (int p = 0; p < P; ++p) {
-        if (devs[p] != devs[0]) same = false;
-        for (int q = 0; q < p; ++q)
-            if (devs[p] == devs[q]) distinct = false;
-    }
-    if (!same && !distinct)
-        throw Error(TRITD_ERR_ARG, "a device set is distinct devices or one device repeated");
-    for (int d : devs) pick_device(d);
-    if (distinct && P > 1) group_comms(devs);
-
-    hipStream_t vst = nullptr;  // the shared stream of virtual shards
-    struct StreamGuard {
-        hipStream_t s = nullptr;
-        ~StreamGuard() {
-            if (s) (void)hipStreamDestroy(s);
+// A device set driven from the calling thread (SURVEY.md §8b Threading):
+// distinct devices reduce with one grouped ncclAllReduce per buffer over the
+// shards' streams; one device repeated (virtual shards: the sharded schedule
+// on one GPU) sums the shards' buffers on a shared stream instead.
+struct DeviceGroup {
+    std::vector<int> devs;
+    bool same = true;
+    hipStream_t vst = nullptr;  // shared stream of virtual shards
+    DeviceGroup(const std::vector<int>& d, int64_t n1) : devs(d) {
+        const int P = (int)devs.size();
+        if (P < 1 || P > 16) throw Error(TRITD_ERR_ARG, "a device set holds 1..16 devices");
+        if (P > n1) throw Error(TRITD_ERR_ARG, "more shards than mode-1 rows");
+        bool distinct = true;
+        for (int p = 0; p < P; ++p) {
+            if (devs[p] != devs[0]) same = false;
+            for (int q = 0; q < p; ++q)
+                if (devs[p] == devs[q]) distinct = false;
         }
-    } sg;
-    if (same && P > 1) {
-        TRITD_HIP(hipSetDevice(devs[0]));
-        TRITD_HIP(hipStreamCreateWithFlags(&vst, hipStreamNonBlocking));
-        sg.s = vst;
+        if (!same && !distinct)
+            throw Error(TRITD_ERR_ARG, "a device set is distinct devices or one device repeated");
+        for (int dv : devs) pick_device(dv);
+        if (distinct && P > 1) group_comms(devs);
+        if (same && P > 1) {
+            TRITD_HIP(hipSetDevice(devs[0]));
+            TRITD_HIP(hipStreamCreateWithFlags(&vst, hipStreamNonBlocking));
+        }
     }
-    std::vector<std::unique_ptr<Session>> ss;
-    for (int p = 0; p < P; ++p) {  // balanced rows: every shard non-empty
-        const int64_t i0 = n1 * p / P, i1 = n1 * (p + 1) / P;
-        TRITD_HIP(hipSetDevice(devs[p]));
-        ss.emplace_back(new Session(devs[p], static_cast<const char*>(D) + i0 * es, n1, n1, n2, n3,
-                                    i0, i1, r, o, A0, B0, C0, nullptr, flags, vst,
-                                    /*defer_normD=*/true));
+    ~DeviceGroup() {
+        if (vst) (void)hipStreamDestroy(vst);
     }
-    std::vector<double*> b(P);
-    auto reduce = [&](double* (Session::*get)(), int64_t count) {
+    int size() const { return (int)devs.size(); }
+    // balanced rows: every shard non-empty
+    std::pair<int64_t, int64_t> rows(int p, int64_t n1) const {
+        return {n1 * p / size(), n1 * (p + 1) / size()};
+    }
+    // in-place sum of buf[p] (count doubles on device p, stream st[p]) over p
+    void reduce(const std::vector<double*>& buf, const std::vector<hipStream_t>& st,
+                int64_t count) const {
+        const int P = size();
         if (P == 1) return;
-        for (int p = 0; p < P; ++p) b[p] = ((*ss[p]).*get)();
         if (same) {
-            launch_vsum(b.data(), P, count, vst);
+            launch_vsum(const_cast<double* const*>(buf.data()), P, count, vst);
             return;
         }
         ncclResult_t rr = ncclGroupStart();
         for (int p = 0; p < P && rr == ncclSuccess; ++p) {
             TRITD_HIP(hipSetDevice(devs[p]));
-            rr = ncclAllReduce(b[p], b[p], (size_t)count, ncclFloat64, ncclSum, g_comms[p],
-                               ss[p]->stream());
+            rr = ncclAllReduce(buf[p], buf[p], (size_t)count, ncclFloat64, ncclSum, g_comms[p], st[p]);
         }
         const ncclResult_t re = ncclGroupEnd();
         if (rr != ncclSuccess || re != ncclSuccess)
             throw Error(TRITD_ERR_RCCL, std::string("grouped ncclAllReduce: ") +
                                             ncclGetErrorString(rr != ncclSuccess ? rr : re));
-    };
-    auto each = [&](auto&& f) {
+    }
+    // reduce a per-session buffer (member function `get`) over all shards
+    template <class S>
+    void reduce(std::vector<std::unique_ptr<S>>& ss, double* (S::*get)(), int64_t count) const {
+        std::vector<double*> b;
+        std::vector<hipStream_t> st;
+        for (auto& s : ss) {
+            b.push_back(((*s).*get)());
+            st.push_back(s->stream());
+        }
+        reduce(b, st, count);
+    }
+    template <class S, class F>
+    static void each(std::vector<std::unique_ptr<S>>& ss, F&& f) {
         for (auto& s : ss) {
             TRITD_HIP(hipSetDevice(s->device()));
             f(*s);
         }
-    };
-    reduce(&Session::red3, 2);
+    }
+};
+
+// One ADMM problem sharded along mode 1 over `devs`: every
+// iteration runs the four phases of solver.cpp on each shard with the three
+// reductions between them.  D, O, E are column-major n1 x n2 x n3 host arrays
+// of es-byte elements.
+void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t flags, int64_t n1,
+               int64_t n2, int64_t n3, int32_t r, const tritd_opts& o, const double* A0,
+               const double* B0, const double* C0, double* A, double* B, double* C, void* O,
+               void* E, double* errHist, int32_t* iters) {
+    DeviceGroup grp(devs, n1);
+    const int P = grp.size();
+    std::vector<std::unique_ptr<Session>> ss;
+    for (int p = 0; p < P; ++p) {
+        const auto [i0, i1] = grp.rows(p, n1);
+        TRITD_HIP(hipSetDevice(devs[p]));
+        ss.emplace_back(new Session(devs[p], static_cast<const char*>(D) + i0 * es, n1, n1, n2, n3,
+                                    i0, i1, r, o, A0, B0, C0, nullptr, flags, grp.vst,
+                                    /*defer_normD=*/true));
+    }
+    auto each = [&](auto&& f) { DeviceGroup::each(ss, f); };
+    grp.reduce(ss, &Session::red3, 2);
     each([](Session& s) { s.set_normD_from_red3(); });
     for (int it = 0; it < o.maxIter; ++it) {
         int k = 0;
         each([&](Session& s) { k = s.next_iter(); });
         if (!k) break;
         each([&](Session& s) { s.phaseA(k); });
-        reduce(&Session::red1, ss[0]->red1_count());
+        grp.reduce(ss, &Session::red1, ss[0]->red1_count());
         each([&](Session& s) { s.phaseB(k); });
-        reduce(&Session::red2, ss[0]->red2_count());
+        grp.reduce(ss, &Session::red2, ss[0]->red2_count());
         each([&](Session& s) { s.phaseC(k); });
-        reduce(&Session::red3, 2);
+        grp.reduce(ss, &Session::red3, 2);
         each([&](Session& s) { s.phaseD(k); });
         TRITD_HIP(hipSetDevice(devs[0]));
         ss[0]->maybe_print(k);
@@ -206,6 +239,47 @@ void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t 
         ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr,
                    O ? static_cast<char*>(O) + i0 * es : nullptr,
                    E ? static_cast<char*>(E) + i0 * es : nullptr, n1, p == 0 ? errHist : nullptr, &k);
+    }
+    if (iters) *iters = k;
+}
+
+// triple_decomp_ALS over a device set: the ALS phases (als.cpp) with the
+// fit sum, [M2 | A^TA] and M3 reduced between them.
+void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, int64_t n2,
+                   int64_t n3, int32_t r, int maxIter, double tol, const double* A0,
+                   const double* B0, const double* C0, double* A, double* B, double* C,
+                   double* errHist, int32_t* iters) {
+    DeviceGroup grp(devs, n1);
+    const int P = grp.size();
+    std::vector<std::unique_ptr<AlsSession>> ss;
+    for (int p = 0; p < P; ++p) {
+        const auto [i0, i1] = grp.rows(p, n1);
+        TRITD_HIP(hipSetDevice(devs[p]));
+        ss.emplace_back(new AlsSession(devs[p], X + i0, n1, n1, n2, n3, i0, i1, r, maxIter, tol, A0,
+                                       B0, C0, nullptr, 0, grp.vst, /*defer_norm=*/true));
+    }
+    auto each = [&](auto&& f) { DeviceGroup::each(ss, f); };
+    grp.reduce(ss, &AlsSession::red0, 2);
+    each([](AlsSession& s) { s.set_norm_from_red0(); });
+    for (int it = 0; it < maxIter; ++it) {
+        int k = 0;
+        each([&](AlsSession& s) { k = s.next_iter(); });
+        if (!k) break;
+        each([&](AlsSession& s) { s.phaseFit(k); });
+        grp.reduce(ss, &AlsSession::red0, 2);
+        each([&](AlsSession& s) { s.phaseErr(k); });
+        TRITD_HIP(hipSetDevice(devs[0]));
+        ss[0]->maybe_print(k);
+        each([&](AlsSession& s) { s.phaseA(k); });
+        grp.reduce(ss, &AlsSession::red1, ss[0]->red1_count());
+        each([&](AlsSession& s) { s.phaseB(k); });
+        grp.reduce(ss, &AlsSession::red2, ss[0]->red2_count());
+        each([&](AlsSession& s) { s.phaseC(k); });
+    }
+    int k = 0;
+    for (int p = 0; p < P; ++p) {
+        TRITD_HIP(hipSetDevice(devs[p]));
+        ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, p == 0 ? errHist : nullptr, &k);
     }
     if (iters) *iters = k;
 }
@@ -483,6 +557,122 @@ void tritd_shutdown(void) {
     drop_comms();
     g_devices.clear();
 }
+
+// ---------------------------------------------------------------------------
+// ALS variant (triple_decomp_ALS.m)
+// ---------------------------------------------------------------------------
+tritd_status tritd_als_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                           const tritd_opts* opts, const double* A0, const double* B0,
+                           const double* C0, double* A, double* B, double* C, double* errHist,
+                           int32_t* iters, int32_t device) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        check_als_opts(opts);
+        check_dims(n1, n2, n3, r);
+        need(X, "X"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        const int maxIter = opts->maxIter < 0 ? 0 : opts->maxIter;
+        if (device < 0 && g_devices.size() > 1) {
+            run_als_group(g_devices, X, n1, n2, n3, r, maxIter, opts->tol, A0, B0, C0, A, B, C,
+                          errHist, iters);
+            return;
+        }
+        const int dev = pick_device(device < 0 && !g_devices.empty() ? g_devices[0] : device);
+        AlsSession s(dev, X, n1, n1, n2, n3, 0, n1, r, maxIter, opts->tol, A0, B0, C0, nullptr, 0);
+        s.run(maxIter);
+        int k = 0;
+        s.get(A, B, C, errHist, &k);
+        if (iters) *iters = k;
+    });
+}
+
+tritd_status tritd_als_sharded_virtual_f64(const double* X, int64_t n1, int64_t n2, int64_t n3,
+                                           int32_t r, const tritd_opts* opts, const double* A0,
+                                           const double* B0, const double* C0, int32_t nshards,
+                                           double* A, double* B, double* C, double* errHist,
+                                           int32_t* iters, int32_t device) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        check_als_opts(opts);
+        check_dims(n1, n2, n3, r);
+        need(X, "X"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        if (nshards < 1 || nshards > 16 || nshards > n1)
+            throw Error(TRITD_ERR_ARG, "nshards must be in 1..min(16,n1)");
+        const int dev = pick_device(device);
+        run_als_group(std::vector<int>(nshards, dev), X, n1, n2, n3, r,
+                      opts->maxIter < 0 ? 0 : opts->maxIter, opts->tol, A0, B0, C0, A, B, C,
+                      errHist, iters);
+    });
+}
+
+tritd_status tritd_als_session_create(tritd_als_session** out, int32_t device, const double* X,
+                                      int64_t ldX, int64_t n1, int64_t n2, int64_t n3, int64_t i0,
+                                      int64_t i1, int32_t r, const tritd_opts* opts,
+                                      const double* A0, const double* B0, const double* C0,
+                                      tritd_comm* comm, uint32_t flags, int32_t quiet) {
+    return guarded([&] {
+        need(out, "out");
+        *out = nullptr;
+        check_als_opts(opts);
+        check_dims(n1, n2, n3, r);
+        need(X, "X"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        if (flags & ~(uint32_t)TRITD_SESSION_D_ON_DEVICE)
+            throw Error(TRITD_ERR_UNSUPPORTED, "ALS sessions are fp64 (flags: D_ON_DEVICE only)");
+        if (i0 < 0 || i1 > n1 || i0 >= i1) throw Error(TRITD_ERR_ARG, "bad shard range");
+        if (ldX < i1 - i0) throw Error(TRITD_ERR_ARG, "ldX smaller than the shard");
+        const int dev = pick_device(device);
+        auto* s = new AlsSession(dev, X, ldX, n1, n2, n3, i0, i1, r,
+                                 opts->maxIter < 0 ? 0 : opts->maxIter, opts->tol, A0, B0, C0,
+                                 comm, flags);
+        s->set_quiet(quiet != 0);
+        *out = reinterpret_cast<tritd_als_session*>(s);
+    });
+}
+
+tritd_status tritd_als_session_run(tritd_als_session* s, int32_t iters) {
+    return guarded([&] {
+        need(s, "session");
+        reinterpret_cast<AlsSession*>(s)->run(iters);
+    });
+}
+
+tritd_status tritd_als_session_sync(tritd_als_session* s, int32_t* iters_done, int32_t* stopped) {
+    return guarded([&] {
+        need(s, "session");
+        int d = 0, st = 0;
+        reinterpret_cast<AlsSession*>(s)->sync(&d, &st);
+        if (iters_done) *iters_done = d;
+        if (stopped) *stopped = st;
+    });
+}
+
+tritd_status tritd_als_session_get(tritd_als_session* s, double* A, double* B, double* C,
+                                   double* errHist, int32_t* iters) {
+    return guarded([&] {
+        need(s, "session");
+        int k = 0;
+        reinterpret_cast<AlsSession*>(s)->get(A, B, C, errHist, &k);
+        if (iters) *iters = k;
+    });
+}
+
+tritd_status tritd_als_session_set_timing(tritd_als_session* s, int32_t enable) {
+    return guarded([&] {
+        need(s, "session");
+        reinterpret_cast<AlsSession*>(s)->set_timing(enable != 0);
+    });
+}
+
+tritd_status tritd_als_session_kernel_ms(tritd_als_session* s, double* fit_ms, double* mode3_ms,
+                                         double* iteration_ms, int32_t* samples) {
+    return guarded([&] {
+        need(s, "session");
+        int n = 0;
+        reinterpret_cast<AlsSession*>(s)->kernel_ms(fit_ms, mode3_ms, iteration_ms, &n);
+        if (samples) *samples = n;
+    });
+}
+
+void tritd_als_session_destroy(tritd_als_session* s) { delete reinterpret_cast<AlsSession*>(s); }
 
 // ---------------------------------------------------------------------------
 // primitives

@@ -1,0 +1,220 @@
+// Kernels of the ALS variant, fast_robust_triple_tensor/triple_decomp_ALS.m
+// (DESIGN.md §8).
+//
+// One ALS iteration k reads the fixed data tensor X twice:
+//   k_als_fit   Xhat = triple_product(A,B,C)            triple_decomp_ALS.m:15 (never stored)
+//               ||X(:) - Xhat(:)||^2                     :16
+//               W(ij,k) = sum_t X(ij,t) C^(t,k)          mode-1/2 half of :26-27 and :31-32
+//               (C^ is the C of iteration k for both: B is updated with the
+//               new A but the old C, :30-32)
+//   K2 (k_m3)   X3 * H'                                  :36-37, over the TX copy of X
+// plus the small M1 / M2 / Gram / solve / apply kernels the ADMM shares.
+// k_als_fit is K5 without the ADMM elementwise chain: one wave per ij-tile
+// walking its t-tiles (X tile-major, common.h), tile tt+1 prefetched while
+// tile tt is computed, L and W on v_mfma_f64_16x16x4_f64 with C^ staged per
+// workgroup in LDS.  Algorithmic traffic N*8 B read + W written.
+#include "kernels.h"
+
+namespace tritd {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+static constexpr int FIT_WAVES = 4;
+
+__device__ __forceinline__ d4 als_mfma4(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int RP>
+__global__ __launch_bounds__(64 * FIT_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_als_fit(AlsFitArgs a) {
+    if (*a.stop) return;
+    constexpr int KS = RP / 4;    // K-steps of the L MFMA
+    constexpr int MT = RP / 16;   // k-tiles of W
+    constexpr int LDC = RP + 16;  // padded row stride of the [t][k] slice
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int il = lane & 15;
+    const int tg = lane >> 4;
+    const int64_t tile = (int64_t)blockIdx.x * FIT_WAVES + wid;
+    const bool active = tile < a.tiles;
+    const int64_t qper = a.n1p >> 4;
+    const int64_t j = active ? tile / qper : 0;
+    const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
+    const int64_t ntt = a.ntt;
+
+    __shared__ double sCT[2][RP * 16];   // L operand  C^(t0 + l&15, 4s + l>>4)
+    __shared__ double sC[2][16 * LDC];   // W operand  C^(t0 + 4r + l>>4, 16m + l&15)
+    constexpr int SP = 16 * RP / 2;
+    constexpr int NS = (SP + 64 * FIT_WAVES - 1) / (64 * FIT_WAVES);
+    d2v sv[NS];
+    auto stage_load = [&](int64_t tt) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 64 * FIT_WAVES;
+            if (SP % (64 * FIT_WAVES) == 0 || e < SP)
+                sv[q] = *reinterpret_cast<const d2v*>(a.Ch + (tt << 4) * RP + 2 * e);
+        }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 64 * FIT_WAVES;
+            if (SP % (64 * FIT_WAVES) == 0 || e < SP) {
+                const int row = (2 * e) / RP, k = (2 * e) % RP;
+                sC[buf][row * LDC + k] = sv[q][0];
+                sC[buf][row * LDC + k + 1] = sv[q][1];
+                sCT[buf][k * 16 + row] = sv[q][0];
+                sCT[buf][(k + 1) * 16 + row] = sv[q][1];
+            }
+        }
+    };
+
+    double kr[KS];  // (A^ o B^)(ij, 4s + l>>4): the Khatri-Rao row of this lane's ij
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int k = 4 * s + tg;
+        kr[s] = active ? a.Ah[i * RP + k] * a.Bh[j * RP + k] : 0.0;
+    }
+    d4 wacc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wacc[m] = d4{0.0, 0.0, 0.0, 0.0};
+    double ss = 0.0;
+    const d2v* X2 = reinterpret_cast<const d2v*>(a.X);
+
+    // Two named register sets, the t-walk unrolled by two (a copy cur = next
+    // would make the compiler wait for the prefetch at the copy; k_admm.hip).
+    struct Regs {
+        d2v x[2];
+    };
+    auto load = [&](int64_t tt, Regs& nx) {
+        const int64_t o = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
+        nx.x[0] = X2[o];
+        nx.x[1] = X2[o + 64];
+    };
+    auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+        if (pf) {
+            stage_load(tt + 1);
+            load(tt + 1, nx);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const double* cT = sCT[buf];
+        const double* cR = sC[buf];
+        d4 lacc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) lacc = als_mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
+        double xr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            xr[r] = cx.x[r >> 1][r & 1];
+            const double d = xr[r] - lacc[r];  // X(:) - Xhat(:)
+            ss += d * d;
+        }
+        // W^T(k, ij) += sum_t C^(t,k) X(t, ij): the C/D register r of the X
+        // tile (t = t0 + 4r + l>>4, ij = l&15) is directly the B operand
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                wacc[m] = als_mfma4(cR[(4 * r + tg) * LDC + 16 * m + il], xr[r], wacc[m]);
+        if (pf) stage_store(buf ^ 1);
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    Regs xa, xb;
+    xa.x[0] = xa.x[1] = xb.x[0] = xb.x[1] = d2v{0.0, 0.0};
+    load(0, xa);
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    int64_t tt = 0;
+    for (; tt + 2 < ntt; tt += 2) {
+        body(tt, 0, xa, xb, true);
+        body(tt + 1, 1, xb, xa, true);
+    }
+    if (tt + 1 < ntt) {
+        body(tt, 0, xa, xb, true);
+        body(tt + 1, 1, xb, xa, false);
+    } else {
+        body(tt, 0, xa, xb, false);
+    }
+    if (active) {
+        const int64_t wbase = (tile << 4) + il;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                a.Wk[(int64_t)(16 * m + tg + 4 * rr) * a.plane + wbase] = wacc[m][rr];
+    }
+    // fixed-order block reduction (pairs: the second is 0, k_reduce_pairs)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+    __shared__ double red[FIT_WAVES];
+    if (lane == 0) red[wid] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double x = 0.0;
+        for (int w = 0; w < FIT_WAVES; ++w) x += red[w];
+        a.partial[2 * blockIdx.x] = x;
+        a.partial[2 * blockIdx.x + 1] = 0.0;
+    }
+}
+
+int als_fit_grid(const Geom& g) { return (int)cdiv(g.tiles, FIT_WAVES); }
+
+void launch_als_fit(const Geom& g, const AlsFitArgs& a, hipStream_t st) {
+    const dim3 grid(als_fit_grid(g)), block(64 * FIT_WAVES);
+    switch (g.RP) {
+        case 16: hipLaunchKernelGGL(k_als_fit<16>, grid, block, 0, st, a); break;
+        case 32: hipLaunchKernelGGL(k_als_fit<32>, grid, block, 0, st, a); break;
+        case 48: hipLaunchKernelGGL(k_als_fit<48>, grid, block, 0, st, a); break;
+        case 64: hipLaunchKernelGGL(k_als_fit<64>, grid, block, 0, st, a); break;
+        default: throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by the ALS fit kernel");
+    }
+    TRITD_CHECK_LAUNCH();
+}
+
+// errHist(k) = norm(X(:) - Xhat(:)) / Xnorm and the stop test of
+// triple_decomp_ALS.m:16,20-23.  ctrl[0] = stop (set BEFORE the update of
+// iteration k, so the update kernels of k early-exit and A, B, C stay those
+// of iteration k), ctrl[1] = entries of errHist.
+__global__ void k_als_finish(const double* ss, double Xnorm, int k, double tol, double* errHist,
+                             int* ctrl) {
+    if (ctrl[0]) return;
+    const double e = sqrt(ss[0]) / Xnorm;
+    errHist[k - 1] = e;
+    ctrl[1] = k;
+    if (k > 1 && fabs(e - errHist[k - 2]) < tol * errHist[k - 2]) ctrl[0] = 1;
+}
+
+void launch_als_finish(const double* ss, double Xnorm, int k, double tol, double* errHist,
+                       int* ctrl, hipStream_t st) {
+    hipLaunchKernelGGL(k_als_finish, dim3(1), dim3(1), 0, st, ss, Xnorm, k, tol, errHist, ctrl);
+    TRITD_CHECK_LAUNCH();
+}
+
+// Tile-major -> TX (the B-operand order of K2, common.h), tile by tile:
+// TX slot (s, l) at (s>>1)*128 + 2l + (s&1) holds (i%16 = 4s + l>>4,
+// t%16 = l&15).  One-off per ALS solve (X is fixed).
+__global__ __launch_bounds__(256) void k_tm_to_tx(const double* __restrict__ src,
+                                                  double* __restrict__ dst, int64_t Ntm) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < Ntm;
+         e += (int64_t)gridDim.x * 256) {
+        const int w = (int)(e & 255);
+        const int s = ((w >> 7) << 1) | (w & 1), l = (w & 127) >> 1;
+        const int il = 4 * s + (l >> 4), tl = l & 15;  // element of this TX slot
+        const int r = tl >> 2, lm = ((tl & 3) << 4) | il;   // its TM slot
+        dst[e] = src[(e & ~(int64_t)255) + ((r >> 1) << 7) + (lm << 1) + (r & 1)];
+    }
+}
+
+void launch_tm_to_tx(const Geom& g, const double* src, double* dst, hipStream_t st) {
+    int64_t b = cdiv(g.Ntm, 256);
+    if (b > 16384) b = 16384;
+    hipLaunchKernelGGL(k_tm_to_tx, dim3((unsigned)b), dim3(256), 0, st, src, dst, g.Ntm);
+    TRITD_CHECK_LAUNCH();
+}
+
+}  // namespace tritd

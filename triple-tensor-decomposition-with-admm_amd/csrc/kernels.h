@@ -94,6 +94,23 @@ void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hi
 void launch_design(char which, const double* P, const double* Q, int64_t nP, int64_t nQ, int r,
                    double* out, hipStream_t st);
 
+// ---- ALS variant (k_als.hip; triple_decomp_ALS.m) --------------------------
+struct AlsFitArgs {
+    const double* X;   // tile-major data tensor
+    double* Wk;        // W = X x3 C^ (planes of n1p*n2)
+    const double* Ah;
+    const double* Bh;
+    const double* Ch;
+    double* partial;   // [grid][2]: sum (X - Xhat)^2, 0
+    int64_t n1p, n2, n3p, plane, tiles, ntt;
+    const int* stop;
+};
+int als_fit_grid(const Geom& g);
+void launch_als_fit(const Geom& g, const AlsFitArgs& a, hipStream_t st);
+void launch_als_finish(const double* ss, double Xnorm, int k, double tol, double* errHist,
+                       int* ctrl, hipStream_t st);
+void launch_tm_to_tx(const Geom& g, const double* src, double* dst, hipStream_t st);
+
 // ---------------------------------------------------------------------------
 // fp32 data path (D of class single): T, O, E, Y_L, Y_O, W and
 // the mode contractions in fp32; factors, Grams and solves in fp64.

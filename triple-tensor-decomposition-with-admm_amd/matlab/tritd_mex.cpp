@@ -4,6 +4,8 @@
 //                         D double -> tritd_admm_f64; D single -> tritd_admm_f32
 //                         (O, E single; A, B, C, errHist double: MATLAB's class
 //                         rules for a single D)
+//   [A,B,C,errHist] = tritd_mex('als', X, r, opts, A0, B0, C0)
+//                         triple_decomp_ALS (double X) -> tritd_als_f64
 //   tritd_mex('devices', idx)  HIP device ordinals (0-based) the next solves
 //                         shard D over (tritd_set_devices; [] clears)
 //   X  = tritd_mex('triple_product', A, B, C)
@@ -11,7 +13,7 @@
 //   Y  = tritd_mex('soft_threshold', X, lam)
 //
 // Called by the drop-in wrappers in this folder (triple_decomp_ADMM.m,
-// triple_decomp_ADMM_outlier.m, triple_product.m), which shadow
+// triple_decomp_ADMM_outlier.m, triple_decomp_ALS.m, triple_product.m), which shadow
 // fast_robust_triple_tensor/*.m when this folder is first on the path.
 // Conventions follow the only MEX in the reference tree
 // (other_methods/.../proximal_operator/flsa.c:113-142): double inputs via
@@ -152,6 +154,68 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     }
 }
 
+// triple_decomp_ALS.m:2-3 reads opts.maxIter, then opts.tol (nothing else)
+bool read_als_opts(const mxArray* s, tritd_opts* o, std::string* err) {
+    std::memset(o, 0, sizeof *o);
+    if (!mxIsStruct(s)) {
+        *err = "opts must be a struct";
+        return false;
+    }
+    const mxArray* mi = mxGetField(s, 0, "maxIter");
+    if (!mi) {
+        *err = "Reference to non-existent field 'maxIter'.";
+        return false;
+    }
+    const mxArray* tl = mxGetField(s, 0, "tol");
+    if (!tl) {
+        *err = "Reference to non-existent field 'tol'.";
+        return false;
+    }
+    o->maxIter = (int32_t)mxGetScalar(mi);
+    o->tol = mxGetScalar(tl);
+    o->present = TRITD_OPT_MAXITER | TRITD_OPT_TOL;
+    return true;
+}
+
+void do_als(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs != 7) fail("tritd:nargin", "usage: tritd_mex('als', X, r, opts, A0, B0, C0)");
+    need_double(prhs[1], "X");
+    int64_t n[3];
+    std::string err;
+    if (!size3(prhs[1], n, &err)) fail("tritd:dims", err);
+    const int32_t r = (int32_t)mxGetScalar(prhs[2]);
+    tritd_opts o;
+    if (!read_als_opts(prhs[3], &o, &err)) fail("MATLAB:nonExistentField", err);
+    for (int k = 4; k < 7; ++k) need_double(prhs[k], "initial factor");
+    const int64_t R = (int64_t)r * r;
+    if ((int64_t)mxGetNumberOfElements(prhs[4]) != n[0] * R ||
+        (int64_t)mxGetNumberOfElements(prhs[5]) != R * n[1] ||
+        (int64_t)mxGetNumberOfElements(prhs[6]) != R * n[2])
+        fail("tritd:dims", "A0, B0, C0 must be n1 x r x r, r x n2 x r, r x r x n3");
+    mxArray* A = make3(n[0], r, r);
+    mxArray* B = make3(r, n[1], r);
+    mxArray* C = make3(r, r, n[2]);
+    mxArray* eh = mxCreateDoubleMatrix(o.maxIter > 0 ? o.maxIter : 0, 1, mxREAL);
+    int32_t k = 0;
+    tritd_set_print_callback(print_line, nullptr);
+    const tritd_status st = tritd_als_f64(mxGetPr(prhs[1]), n[0], n[1], n[2], r, &o,
+                                          mxGetPr(prhs[4]), mxGetPr(prhs[5]), mxGetPr(prhs[6]),
+                                          mxGetPr(A), mxGetPr(B), mxGetPr(C),
+                                          o.maxIter > 0 ? mxGetPr(eh) : nullptr, &k, -1);
+    if (st != TRITD_OK) {
+        for (mxArray* x : {A, B, C, eh}) mxDestroyArray(x);
+        fail(st == TRITD_ERR_OPTS ? "MATLAB:nonExistentField" : "tritd:solver", status_msg(st));
+    }
+    mxSetM(eh, (mwSize)k);  // errHist = errHist(1:k)  (triple_decomp_ALS.m:21)
+    mxArray* outs[4] = {A, B, C, eh};
+    for (int q = 0; q < 4; ++q) {
+        if (q < (nlhs > 0 ? nlhs : 1))
+            plhs[q] = outs[q];
+        else
+            mxDestroyArray(outs[q]);
+    }
+}
+
 void do_devices(int, mxArray*[], int nrhs, const mxArray* prhs[]) {
     if (nrhs != 2) fail("tritd:nargin", "usage: tritd_mex('devices', idx)");
     need_double(prhs[1], "idx");
@@ -233,6 +297,8 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         do_devices(nlhs, plhs, nrhs, prhs);
     else if (c == "admm")
         do_admm(nlhs, plhs, nrhs, prhs);
+    else if (c == "als")
+        do_als(nlhs, plhs, nrhs, prhs);
     else if (c == "triple_product")
         do_triple_product(nlhs, plhs, nrhs, prhs);
     else if (c == "unfold")

@@ -8,6 +8,7 @@ Import with the package directory on sys.path:
 """
 from ._lib import LIB_PATH, TritdError, device_count, set_devices, set_printer, shutdown  # noqa: F401
 from .api import (  # noqa: F401
+    AlsSession,
     Comm,
     Session,
     buildF,
@@ -18,6 +19,7 @@ from .api import (  # noqa: F401
     soft_threshold,
     triple_decomp_ADMM,
     triple_decomp_ADMM_outlier,
+    triple_decomp_ALS,
     triple_product,
     unfold,
 )

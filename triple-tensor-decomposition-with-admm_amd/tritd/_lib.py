@@ -75,6 +75,18 @@ SIGNATURES = {
                                                  i32]),
     "tritd_set_devices": (C.c_int, [C.POINTER(i32), i32]),
     "tritd_shutdown": (None, []),
+    "tritd_als_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp, vp, vp, vp,
+                                vp, C.POINTER(i32), i32]),
+    "tritd_als_session_create": (C.c_int, [C.POINTER(vp), i32, vp, i64, i64, i64, i64, i64, i64,
+                                           i32, C.POINTER(Opts), vp, vp, vp, vp, C.c_uint32, i32]),
+    "tritd_als_session_run": (C.c_int, [vp, i32]),
+    "tritd_als_session_sync": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32)]),
+    "tritd_als_session_get": (C.c_int, [vp, vp, vp, vp, vp, C.POINTER(i32)]),
+    "tritd_als_session_set_timing": (C.c_int, [vp, i32]),
+    "tritd_als_session_kernel_ms": (C.c_int, [vp, dp, dp, dp, C.POINTER(i32)]),
+    "tritd_als_session_destroy": (None, [vp]),
+    "tritd_als_sharded_virtual_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp,
+                                                i32, vp, vp, vp, vp, C.POINTER(i32), i32]),
     "tritd_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp]),
     "tritd_unfold_f64": (C.c_int, [vp, i64, i64, i64, i32, vp]),
     "tritd_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp]),

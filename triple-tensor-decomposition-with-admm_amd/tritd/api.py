@@ -5,6 +5,7 @@ the MATLAB file it replaces and runs on the GPU through libtritd.so:
 
     triple_decomp_ADMM(D, r, opts)          fast_robust_triple_tensor/triple_decomp_ADMM.m:1
     triple_decomp_ADMM_outlier(D, r, opts)  alias expected at video_triple_comparison.m:54
+    triple_decomp_ALS(X, r, opts)           fast_robust_triple_tensor/triple_decomp_ALS.m:1
     triple_product(A, B, C)                 triple_product.m:1
     unfold(X, mode)                         unfold.m:1
     soft_threshold(X, lam)                  soft_threshold.m:1
@@ -167,6 +168,57 @@ def _admm_f32(D, r, o, opts, A0, B0, C0, device, return_E, return_iters):
 triple_decomp_ADMM_outlier = triple_decomp_ADMM
 
 
+def make_als_opts(opts):
+    """opts of triple_decomp_ALS.m:2-3 (only maxIter and tol are read, in
+    that order; a missing one raises like MATLAB, everything else is ignored)."""
+    o = _lib.Opts()
+    for name in ("maxIter", "tol"):
+        if _get(opts, name) is None:
+            raise KeyError(f"Reference to non-existent field '{name}'.")
+    o.maxIter = int(_get(opts, "maxIter"))
+    o.tol = float(_get(opts, "tol"))
+    o.present = _lib.OPT_MAXITER | _lib.OPT_TOL
+    return o
+
+
+def triple_decomp_ALS(X, r, opts, A0=None, B0=None, C0=None, *, device=-1, return_iters=False,
+                      virtual_shards=0):
+    """[A,B,C,errHist] = triple_decomp_ALS(X, r, opts) on the GPU
+    (fast_robust_triple_tensor/triple_decomp_ALS.m:1-40).
+
+    The initial factors are drawn here in the order of :8-10 unless given
+    (MATLAB's randn is not reproducible outside MATLAB).  The progress line of
+    :17-19 goes to the printer (``tritd.set_printer``; stdout by default).
+    ``return_iters`` adds k; ``virtual_shards=P`` runs the mode-1 sharded
+    schedule as P shards on one device.  fp64, r <= 8."""
+    o = make_als_opts(opts)
+    X = _fortran(X)
+    n1, n2, n3 = _size3(X)
+    r = int(r)
+    if A0 is None or B0 is None or C0 is None:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, opts)
+    else:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, dict(A0=A0, B0=B0, C0=C0))
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cf = np.zeros((r, r, n3), order="F")
+    errHist = np.zeros(max(o.maxIter, 1))
+    k = _lib.i32(0)
+    if virtual_shards and virtual_shards > 1:
+        check(lib.tritd_als_sharded_virtual_f64(_ptr(X), n1, n2, n3, r, C.byref(o), _ptr(A0),
+                                                _ptr(B0), _ptr(C0), int(virtual_shards), _ptr(A),
+                                                _ptr(B), _ptr(Cf), _ptr(errHist), C.byref(k),
+                                                int(device)))
+    else:
+        check(lib.tritd_als_f64(_ptr(X), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+                                _ptr(A), _ptr(B), _ptr(Cf), _ptr(errHist), C.byref(k),
+                                int(device)))
+    out = [A, B, Cf, errHist[: k.value].copy()]  # :21 errHist = errHist(1:k)
+    if return_iters:
+        out.append(k.value)
+    return tuple(out)
+
+
 def triple_product(A, B, C_):
     """Xhat = triple_product(A, B, C)  (triple_product.m:1-7)."""
     A = _fortran(A)
@@ -327,6 +379,73 @@ class Session:
             pass
 
 
+class AlsSession:
+    """Steppable device-resident triple_decomp_ALS on one mode-1 shard
+    (bench; one process per GPU with ``comm``).  ``quiet`` drops the
+    every-5-iterations progress line and its host synchronisation."""
+
+    def __init__(self, r, opts, A0, B0, C0, *, n1, n2, n3, i0=0, i1=None, X=None,
+                 x_device_ptr=None, ldX=None, device=0, comm=None, quiet=True):
+        self._s = C.c_void_p()
+        o = make_als_opts(opts)
+        i1 = n1 if i1 is None else i1
+        A0, B0, C0 = _fortran(A0), _fortran(B0), _fortran(C0)
+        flags = 0
+        if x_device_ptr is not None:
+            xptr = C.c_void_p(int(x_device_ptr))
+            flags |= _lib.SESSION_D_ON_DEVICE
+            ldX = ldX if ldX is not None else (i1 - i0)
+        else:
+            X = _fortran(X)
+            xptr = _ptr(X)
+            ldX = ldX if ldX is not None else X.shape[0]
+        self.n1, self.n2, self.n3, self.i0, self.i1, self.r = n1, n2, n3, i0, i1, r
+        self.maxIter = o.maxIter
+        check(lib.tritd_als_session_create(C.byref(self._s), int(device), xptr, int(ldX), n1, n2,
+                                           n3, i0, i1, r, C.byref(o), _ptr(A0), _ptr(B0),
+                                           _ptr(C0), comm.handle if comm is not None else None,
+                                           flags, int(bool(quiet))))
+
+    def run(self, iters):
+        check(lib.tritd_als_session_run(self._s, int(iters)))
+
+    def sync(self):
+        d, s = _lib.i32(0), _lib.i32(0)
+        check(lib.tritd_als_session_sync(self._s, C.byref(d), C.byref(s)))
+        return d.value, bool(s.value)
+
+    def get(self):
+        r, n1, n2, n3 = self.r, self.n1, self.n2, self.n3
+        A = np.zeros((n1, r, r), order="F")
+        B = np.zeros((r, n2, r), order="F")
+        Cf = np.zeros((r, r, n3), order="F")
+        eh = np.zeros(max(self.maxIter, 1))
+        k = _lib.i32(0)
+        check(lib.tritd_als_session_get(self._s, _ptr(A), _ptr(B), _ptr(Cf), _ptr(eh), C.byref(k)))
+        return dict(A=A, B=B, C=Cf, errHist=eh[: k.value].copy(), k=k.value)
+
+    def set_timing(self, on=True):
+        check(lib.tritd_als_session_set_timing(self._s, int(bool(on))))
+
+    def kernel_ms(self):
+        a, b, c = C.c_double(0), C.c_double(0), C.c_double(0)
+        n = _lib.i32(0)
+        check(lib.tritd_als_session_kernel_ms(self._s, C.byref(a), C.byref(b), C.byref(c),
+                                              C.byref(n)))
+        return dict(fit=a.value, mode3=b.value, iteration=c.value, samples=n.value)
+
+    def close(self):
+        if self._s:
+            lib.tritd_als_session_destroy(self._s)
+            self._s = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Comm:
     """RCCL communicator owned by libtritd (one process per GPU)."""
 
@@ -347,6 +466,7 @@ class Comm:
             self.handle = C.c_void_p()
 
 
-__all__ = ["triple_decomp_ADMM", "triple_decomp_ADMM_outlier", "triple_product", "unfold",
+__all__ = ["triple_decomp_ADMM", "triple_decomp_ADMM_outlier", "triple_decomp_ALS", "AlsSession",
+           "make_als_opts", "triple_product", "unfold",
            "soft_threshold", "buildF", "buildG", "buildH", "Session", "Comm", "TritdError",
            "make_opts", "initial_factors"]
