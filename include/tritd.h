@@ -255,6 +255,29 @@ tritd_status tritd_soft_threshold_f64(const double* X, int64_t n, double lam, do
 tritd_status tritd_build_design_f64(char which, const double* P, const double* Q, int64_t nP,
                                     int64_t nQ, int32_t r, double* out);
 
+/* Driver metrics.
+ * evaluate(X, gt, mask) of traffic_triple_comparison.m:194-202 (identical in
+ * video_triple_comparison.m): rmse = norm(X(mask) - gt(:)), nrmse = rmse /
+ * norm(gt(:)).  X has n elements; mask is n bytes (MATLAB logical, nonzero =
+ * true) or NULL for true(size(X)); gt holds m = nnz(mask) elements in
+ * column-major order of the true positions (m = n without a mask) — a
+ * mismatch fails like MATLAB's "Arrays have incompatible sizes".  */
+tritd_status tritd_evaluate_f64(const double* X, int64_t n, const double* gt, int64_t m,
+                                const uint8_t* mask, double* rmse, double* nrmse);
+/* quality_ybz(imagery1, imagery2) (other_methods/Low-rank-.../quality_ybz.m:1-33):
+ * mean over the nf frames (n1 x n2 each; trailing dims folded into nf) of
+ * psnr_index = 10*log10(255^2/mse(x-y)) and ssim_index (Gaussian 11x11
+ * window, sigma 1.5, K = [0.01 0.03], L = 255, 'valid' map; -Inf for frames
+ * smaller than 11x11).  psnr_frames / ssim_frames (nf each) may be NULL. */
+tritd_status tritd_quality_f64(const double* X1, const double* X2, int64_t n1, int64_t n2,
+                               int64_t nf, double* psnr, double* ssim, double* psnr_frames,
+                               double* ssim_frames);
+tritd_status tritd_dev_evaluate_f64(const double* X, int64_t n, const double* gt, int64_t m,
+                                    const uint8_t* mask, double* rmse, double* nrmse, void* stream);
+tritd_status tritd_dev_quality_f64(const double* X1, const double* X2, int64_t n1, int64_t n2,
+                                   int64_t nf, double* psnr, double* ssim, double* psnr_frames,
+                                   double* ssim_frames, void* stream);
+
 /* Device-pointer variants (for device-resident callers and the bench). */
 tritd_status tritd_dev_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t mode,
                                   double* Xn, void* stream);

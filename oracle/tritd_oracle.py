@@ -350,6 +350,75 @@ def evaluate(X, gt, mask=None):
     return rmse, rmse / np.linalg.norm(gt.ravel(order="F"))
 
 
+def fspecial_gaussian(size=11, sigma=1.5):
+    """MATLAB fspecial('gaussian', size, sigma) (Image Processing Toolbox
+    semantics; the toolbox is not in the reference tree): exp(-(x^2+y^2)/2s^2)
+    on a meshgrid, entries below eps*max zeroed, normalised to sum 1."""
+    siz = (size - 1) / 2.0
+    x, y = np.meshgrid(np.arange(-siz, siz + 1), np.arange(-siz, siz + 1))
+    h = np.exp(-(x * x + y * y) / (2.0 * sigma * sigma))
+    h[h < np.finfo(float).eps * h.max()] = 0.0
+    sh = h.sum()
+    return h / sh if sh != 0 else h
+
+
+def filter2_valid(w, img):
+    """filter2(w, img, 'valid'): 2-D correlation over the fully-overlapping positions."""
+    H, W = w.shape
+    M, N = img.shape
+    out = np.zeros((M - H + 1, N - W + 1))
+    for u in range(H):
+        for v in range(W):
+            out += w[u, v] * img[u:u + M - H + 1, v:v + N - W + 1]
+    return out
+
+
+def ssim_index(img1, img2):
+    """other_methods/IPI_RTC_FCTN-main/lib/ssim_index.m with nargin == 2 (the copy
+    `addpath(genpath(pwd))` resolves first; byte-identical to the one in
+    Low-rank-.../ssim_index.m): Gaussian 11x11 sigma 1.5, K = [0.01 0.03],
+    L = 255, mean2 of the 'valid' SSIM map; -Inf below 11x11."""
+    img1 = np.asarray(img1, dtype=np.float64)
+    img2 = np.asarray(img2, dtype=np.float64)
+    M, N = img1.shape
+    if M < 11 or N < 11:
+        return -np.inf
+    w = fspecial_gaussian(11, 1.5)
+    w = w / w.sum(axis=0).sum()
+    C1 = (0.01 * 255) ** 2
+    C2 = (0.03 * 255) ** 2
+    mu1 = filter2_valid(w, img1)
+    mu2 = filter2_valid(w, img2)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1 * mu1, mu2 * mu2, mu1 * mu2
+    sigma1_sq = filter2_valid(w, img1 * img1) - mu1_sq
+    sigma2_sq = filter2_valid(w, img2 * img2) - mu2_sq
+    sigma12 = filter2_valid(w, img1 * img2) - mu1_mu2
+    ssim_map = ((2 * mu1_mu2 + C1) * (2 * sigma12 + C2)) / \
+               ((mu1_sq + mu2_sq + C1) * (sigma1_sq + sigma2_sq + C2))
+    return ssim_map.mean()
+
+
+def psnr_index(x, y):
+    """other_methods/Low-rank-.../psnr_index.m:1-4: 10*log10(255^2/mse(x-y))."""
+    d = np.asarray(x, dtype=np.float64) - np.asarray(y, dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        return 10.0 * np.log10(255.0 ** 2 / np.mean(d * d))
+
+
+def quality_ybz(imagery1, imagery2):
+    """other_methods/Low-rank-.../quality_ybz.m:1-33: mean over frames
+    (trailing dims folded) of psnr_index and ssim_index."""
+    X1 = np.asarray(imagery1, dtype=np.float64)
+    X2 = np.asarray(imagery2, dtype=np.float64)
+    n1, n2 = X1.shape[0], X1.shape[1]
+    X1 = X1.reshape((n1, n2, -1), order="F")
+    X2 = X2.reshape((n1, n2, -1), order="F")
+    nf = X1.shape[2]
+    ps = [psnr_index(X1[:, :, i], X2[:, :, i]) for i in range(nf)]
+    ss = [ssim_index(X1[:, :, i], X2[:, :, i]) for i in range(nf)]
+    return float(np.mean(ps)), float(np.mean(ss))
+
+
 # ---------------------------------------------------------------------------
 # Loop definitions quoted in the reference's comments (known-answer checks)
 # ---------------------------------------------------------------------------

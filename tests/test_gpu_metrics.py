@@ -1,0 +1,70 @@
+"""GPU parity of the driver metrics against the
+oracle restatements: evaluate (traffic_triple_comparison.m:194-202) and
+quality_ybz (psnr_index.m, ssim_index.m).  Tolerances: rmse/nrmse and PSNR
+rtol 1e-12 (fixed-order sums vs numpy's), SSIM rtol 1e-11 (the 11x11 window
+sums are accumulated in a different order than MATLAB's filter2)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tritd():
+    import tritd as t
+    assert t.device_count() > 0, "no GPU visible: the HIP path must run, there is no CPU fallback"
+    return t
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import tritd_oracle
+    return tritd_oracle
+
+
+@pytest.mark.parametrize("shape,p", [((30, 30, 30), 0.1), ((54, 4, 1152), 0.1), ((7, 5, 3), 0.5),
+                                     ((240, 320, 20), 0.05)])
+def test_evaluate_masked_matches_oracle(tritd, orc, shape, p):
+    rng = np.random.default_rng(5)
+    X = np.asfortranarray(rng.standard_normal(shape))
+    Xh = np.asfortranarray(X + 0.01 * rng.standard_normal(shape))
+    mask = rng.random(shape) < p
+    gt = X.ravel(order="F")[mask.ravel(order="F")]          # gt = X(mask_missing)
+    rmse, nrmse = tritd.evaluate(Xh, gt, mask)
+    r_ref, n_ref = orc.evaluate(Xh.ravel(order="F")[mask.ravel(order="F")], gt)
+    assert rmse == pytest.approx(r_ref, rel=1e-12) and nrmse == pytest.approx(n_ref, rel=1e-12)
+    # evaluate(X_hat, X, true(size(X))) -- the driver's RRE
+    rmse, nrmse = tritd.evaluate(Xh, X)
+    r_ref, n_ref = orc.evaluate(Xh, X)
+    assert rmse == pytest.approx(r_ref, rel=1e-12) and nrmse == pytest.approx(n_ref, rel=1e-12)
+
+
+def test_evaluate_size_mismatch_and_empty(tritd):
+    X = np.ones((4, 4, 4))
+    mask = np.zeros(X.shape, dtype=bool)
+    mask[0, 0, 0] = mask[1, 2, 3] = True
+    with pytest.raises(tritd.TritdError, match="incompatible sizes"):
+        tritd.evaluate(X, np.ones(3), mask)
+    r, n = tritd.evaluate(X, np.array([2.0, 1.0]), mask)
+    assert r == 1.0 and n == pytest.approx(1.0 / np.sqrt(5.0), rel=1e-15)
+
+
+@pytest.mark.parametrize("shape", [(40, 50, 4), (240, 320, 6), (11, 11, 2), (64, 17, 3)])
+def test_quality_matches_oracle(tritd, orc, shape):
+    rng = np.random.default_rng(6)
+    X = np.asfortranarray(rng.uniform(0, 255, shape))
+    Y = np.asfortranarray(np.clip(X + rng.normal(0, 12, shape), 0, 255))
+    p, s, pf, sf = tritd.quality_ybz(X, Y, per_frame=True)
+    for f in range(shape[2]):
+        assert pf[f] == pytest.approx(orc.psnr_index(X[:, :, f], Y[:, :, f]), rel=1e-12)
+        assert sf[f] == pytest.approx(orc.ssim_index(X[:, :, f], Y[:, :, f]), rel=1e-11)
+    pr, sr = orc.quality_ybz(X, Y)
+    assert p == pytest.approx(pr, rel=1e-12) and s == pytest.approx(sr, rel=1e-11)
+
+
+def test_quality_edge_cases(tritd):
+    X = np.asfortranarray(np.random.default_rng(7).uniform(0, 255, (10, 30, 2)))
+    p, s = tritd.quality_ybz(X, X + 1.0)
+    assert p == pytest.approx(20 * np.log10(255.0), rel=1e-14) and s == -np.inf
+    p, s = tritd.quality_ybz(np.ones((12, 12, 1)), np.ones((12, 12, 1)))
+    assert p == np.inf and s == 1.0

@@ -233,3 +233,43 @@ def test_als_opts_and_print():
                                            g["B0"], g["C0"], printer=lines.append)
     assert k == 12
     assert lines == ["Iteration %d, relative error = %.4e" % (i, eh[i - 1]) for i in (5, 10)]
+
+
+# ---------------------------------------------------------------------------
+# Driver metrics: evaluate (traffic_triple_comparison.m:194-202), quality_ybz
+# (psnr_index.m, ssim_index.m) — SURVEY.md §8f ranks 1, 3
+# ---------------------------------------------------------------------------
+def test_oracle_filter2_and_window():
+    from scipy.signal import correlate2d
+    w = orc.fspecial_gaussian(11, 1.5)
+    assert w.shape == (11, 11) and abs(w.sum() - 1.0) < 1e-15
+    assert np.array_equal(w, w.T) and np.array_equal(w, w[::-1, ::-1])
+    assert w[5, 5] == w.max()
+    img = np.random.default_rng(1).uniform(0, 255, (23, 19))
+    np.testing.assert_allclose(orc.filter2_valid(w, img), correlate2d(img, w, mode="valid"),
+                               rtol=1e-13)
+
+
+def test_oracle_quality_known_answers():
+    rng = np.random.default_rng(2)
+    X = rng.uniform(0, 255, (20, 24, 3))
+    p, s = orc.quality_ybz(X, X)
+    assert p == np.inf and s == 1.0
+    Y = X + 1.0  # mse = 1 -> psnr = 20 log10(255)
+    p, _ = orc.quality_ybz(X, Y)
+    assert abs(p - 20 * np.log10(255.0)) < 1e-12
+    Z = X + rng.normal(0, 20, X.shape)
+    assert abs(orc.ssim_index(X[:, :, 0], Z[:, :, 0]) - orc.ssim_index(Z[:, :, 0], X[:, :, 0])) < 1e-14
+    assert orc.ssim_index(X[:10, :, 0], Z[:10, :, 0]) == -np.inf  # smaller than the window
+
+
+def test_oracle_evaluate_masked_order():
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((5, 4, 3))
+    Xh = X + 0.1 * rng.standard_normal(X.shape)
+    mask = rng.random(X.shape) < 0.3
+    gt = X[mask.ravel(order="F").reshape(X.shape, order="F")]  # any order of the same set...
+    gt = X.ravel(order="F")[mask.ravel(order="F")]             # ...MATLAB's X(mask) is column-major
+    rmse, nrmse = orc.evaluate(Xh.ravel(order="F")[mask.ravel(order="F")], gt)
+    assert abs(rmse - np.linalg.norm((Xh - X)[mask])) < 1e-14
+    assert abs(nrmse - rmse / np.linalg.norm(X[mask])) < 1e-14

@@ -2,6 +2,8 @@
 // arguments the way the reference fails (missing opts field, bad unfold
 // mode, >3-D data), converts exceptions into tritd_status + a thread-local
 // message, and never writes its inputs.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -282,6 +284,38 @@ void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, in
         ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, p == 0 ? errHist : nullptr, &k);
     }
     if (iters) *iters = k;
+}
+// fspecial('gaussian', 11, 1.5), then ssim_index's window/sum(sum(window));
+// column-major (the window is symmetric)
+std::vector<double> ssim_window() {
+    const int siz = 5;
+    const double sd = 1.5;
+    std::vector<double> h(121);
+    double mx = 0.0;
+    for (int c = 0; c < 11; ++c)
+        for (int r = 0; r < 11; ++r) {
+            const double x = c - siz, y = r - siz;  // [x,y] = meshgrid(-siz:siz)
+            const double v = std::exp(-(x * x + y * y) / (2 * sd * sd));
+            h[c * 11 + r] = v;
+            mx = std::max(mx, v);
+        }
+    for (double& v : h)
+        if (v < 2.220446049250313e-16 * mx) v = 0.0;  // h(h < eps*max(h(:))) = 0
+    for (int pass = 0; pass < 2; ++pass) {  // fspecial's h/sum(h(:)), then ssim_index's sum(sum())
+        double tot = 0.0;
+        if (pass == 0) {
+            for (double v : h) tot += v;
+        } else {
+            for (int c = 0; c < 11; ++c) {
+                double col = 0.0;
+                for (int r = 0; r < 11; ++r) col += h[c * 11 + r];
+                tot += col;
+            }
+        }
+        if (tot != 0.0)
+            for (double& v : h) v /= tot;
+    }
+    return h;
 }
 }  // namespace
 
@@ -798,6 +832,122 @@ tritd_status tritd_build_design_f64(char which, const double* P, const double* Q
         TRITD_HIP(hipMemcpy(dQ.p, Q, dQ.n * 8, hipMemcpyHostToDevice));
         launch_design(which, dP.p, dQ.p, nP, nQ, r, dO.p, nullptr);
         TRITD_HIP(hipMemcpy(out, dO.p, dO.n * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+// ---------------------------------------------------------------------------
+// driver metrics
+// ---------------------------------------------------------------------------
+tritd_status tritd_dev_evaluate_f64(const double* X, int64_t n, const double* gt, int64_t m,
+                                    const uint8_t* mask, double* rmse, double* nrmse,
+                                    void* stream) {
+    return guarded([&] {
+        if (n < 0 || m < 0) throw Error(TRITD_ERR_ARG, "sizes must be >= 0");
+        need(rmse, "rmse"); need(nrmse, "nrmse");
+        if (!mask && m != n) throw Error(TRITD_ERR_ARG, "Arrays have incompatible sizes for this operation.");
+        if (n > 0) { need(X, "X"); }
+        if (m > 0) { need(gt, "gt"); }
+        hipStream_t st = as_stream(stream);
+        double h[2] = {0.0, 0.0};
+        if (n > 0) {
+            const int64_t nb = evaluate_blocks(n);
+            DBuf part, out;
+            part.alloc(2 * (size_t)nb);
+            out.alloc(2);
+            int64_t* sc = nullptr;
+            TRITD_HIP(hipMalloc(&sc, (size_t)(nb + 1) * sizeof(int64_t)));
+            struct Free { int64_t* p; ~Free() { (void)hipFree(p); } } fr{sc};
+            launch_evaluate(X, gt, mask, n, sc, part.p, out.p, sc + nb, st);
+            int64_t total = n;
+            if (mask)
+                TRITD_HIP(hipMemcpyAsync(&total, sc + nb, sizeof total, hipMemcpyDeviceToHost, st));
+            TRITD_HIP(hipMemcpyAsync(h, out.p, sizeof h, hipMemcpyDeviceToHost, st));
+            TRITD_HIP(hipStreamSynchronize(st));
+            // X(mask)-gt(:) with numel(X(mask)) ~= numel(gt) fails in MATLAB
+            // (gt was read only up to m entries: positions past it are not touched
+            // because the check below precedes any use of the sums)
+            if (total != m) throw Error(TRITD_ERR_ARG, "Arrays have incompatible sizes for this operation.");
+        } else if (m != 0) {
+            throw Error(TRITD_ERR_ARG, "Arrays have incompatible sizes for this operation.");
+        }
+        *rmse = std::sqrt(h[0]);
+        *nrmse = *rmse / std::sqrt(h[1]);
+    });
+}
+
+tritd_status tritd_evaluate_f64(const double* X, int64_t n, const double* gt, int64_t m,
+                                const uint8_t* mask, double* rmse, double* nrmse) {
+    return guarded([&] {
+        if (n < 0 || m < 0) throw Error(TRITD_ERR_ARG, "sizes must be >= 0");
+        need(rmse, "rmse"); need(nrmse, "nrmse");
+        if (n > 0) { need(X, "X"); }
+        if (m > 0) { need(gt, "gt"); }
+        pick_device(-1);
+        DBuf dX, dg, dm;
+        dX.alloc((size_t)n);
+        dg.alloc((size_t)m);
+        if (n > 0) TRITD_HIP(hipMemcpy(dX.p, X, (size_t)n * 8, hipMemcpyHostToDevice));
+        if (m > 0) TRITD_HIP(hipMemcpy(dg.p, gt, (size_t)m * 8, hipMemcpyHostToDevice));
+        const uint8_t* dmask = nullptr;
+        if (mask) {
+            dm.alloc_bytes((size_t)n);
+            if (n > 0) TRITD_HIP(hipMemcpy(dm.p, mask, (size_t)n, hipMemcpyHostToDevice));
+            dmask = reinterpret_cast<const uint8_t*>(dm.p);
+        }
+        const tritd_status s = tritd_dev_evaluate_f64(dX.p, n, dg.p, m, dmask, rmse, nrmse, nullptr);
+        if (s != TRITD_OK) throw Error(s, g_last_error);
+    });
+}
+
+
+tritd_status tritd_dev_quality_f64(const double* X1, const double* X2, int64_t n1, int64_t n2,
+                                   int64_t nf, double* psnr, double* ssim, double* psnr_frames,
+                                   double* ssim_frames, void* stream) {
+    return guarded([&] {
+        if (n1 <= 0 || n2 <= 0 || nf <= 0) throw Error(TRITD_ERR_ARG, "sizes must be positive");
+        need(X1, "X1"); need(X2, "X2"); need(psnr, "psnr"); need(ssim, "ssim");
+        hipStream_t st = as_stream(stream);
+        const std::vector<double> w = ssim_window();
+        DBuf dw, scratch, pf, sf;
+        dw.alloc(w.size());
+        TRITD_HIP(hipMemcpyAsync(dw.p, w.data(), w.size() * 8, hipMemcpyHostToDevice, st));
+        scratch.alloc(quality_scratch(n1, n2, nf));
+        pf.alloc((size_t)nf);
+        sf.alloc((size_t)nf);
+        const double C1 = (0.01 * 255) * (0.01 * 255), C2 = (0.03 * 255) * (0.03 * 255);
+        launch_quality(X1, X2, n1, n2, nf, dw.p, C1, C2, scratch.p, pf.p, sf.p, st);
+        std::vector<double> hp((size_t)nf), hs((size_t)nf);
+        TRITD_HIP(hipMemcpyAsync(hp.data(), pf.p, (size_t)nf * 8, hipMemcpyDeviceToHost, st));
+        TRITD_HIP(hipMemcpyAsync(hs.data(), sf.p, (size_t)nf * 8, hipMemcpyDeviceToHost, st));
+        TRITD_HIP(hipStreamSynchronize(st));
+        double mp = 0.0, ms = 0.0;  // mean(): sequential sum / count
+        for (int64_t f = 0; f < nf; ++f) {
+            mp += hp[(size_t)f];
+            ms += hs[(size_t)f];
+        }
+        *psnr = mp / (double)nf;
+        *ssim = ms / (double)nf;
+        if (psnr_frames) std::copy(hp.begin(), hp.end(), psnr_frames);
+        if (ssim_frames) std::copy(hs.begin(), hs.end(), ssim_frames);
+    });
+}
+
+tritd_status tritd_quality_f64(const double* X1, const double* X2, int64_t n1, int64_t n2,
+                               int64_t nf, double* psnr, double* ssim, double* psnr_frames,
+                               double* ssim_frames) {
+    return guarded([&] {
+        if (n1 <= 0 || n2 <= 0 || nf <= 0) throw Error(TRITD_ERR_ARG, "sizes must be positive");
+        need(X1, "X1"); need(X2, "X2"); need(psnr, "psnr"); need(ssim, "ssim");
+        pick_device(-1);
+        const size_t n = (size_t)(n1 * n2 * nf);
+        DBuf a, b;
+        a.alloc(n);
+        b.alloc(n);
+        TRITD_HIP(hipMemcpy(a.p, X1, n * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(b.p, X2, n * 8, hipMemcpyHostToDevice));
+        const tritd_status s = tritd_dev_quality_f64(a.p, b.p, n1, n2, nf, psnr, ssim, psnr_frames,
+                                                     ssim_frames, nullptr);
+        if (s != TRITD_OK) throw Error(s, g_last_error);
     });
 }
 

@@ -111,6 +111,22 @@ void launch_als_finish(const double* ss, double Xnorm, int k, double tol, double
                        int* ctrl, hipStream_t st);
 void launch_tm_to_tx(const Geom& g, const double* src, double* dst, hipStream_t st);
 
+// ---- driver-side metrics (k_metrics.hip) ------------------------------------
+// evaluate (traffic_triple_comparison.m:194-202): out2 = {sum (X(mask)-gt)^2,
+// sum gt^2}; mask may be null (X and gt paired elementwise).  scratch_i64:
+// evaluate_blocks(n) + 1 entries; part: 2*evaluate_blocks(n) doubles; *total
+// receives nnz(mask) (untouched without a mask)
+int64_t evaluate_blocks(int64_t n);
+void launch_evaluate(const double* X, const double* gt, const uint8_t* mask, int64_t n,
+                     int64_t* scratch_i64, double* part, double* out2, int64_t* total,
+                     hipStream_t st);
+// quality_ybz: per-frame psnr/ssim of n1 x n2 x nf tensors; win = the
+// normalised 11x11 Gaussian (column-major, device); scratch: quality_scratch() doubles
+size_t quality_scratch(int64_t n1, int64_t n2, int64_t nf);
+void launch_quality(const double* X, const double* Y, int64_t n1, int64_t n2, int64_t nf,
+                    const double* win, double C1, double C2, double* scratch, double* psnr,
+                    double* ssim, hipStream_t st);
+
 // ---------------------------------------------------------------------------
 // fp32 data path (D of class single): T, O, E, Y_L, Y_O, W and
 // the mode contractions in fp32; factors, Grams and solves in fp64.

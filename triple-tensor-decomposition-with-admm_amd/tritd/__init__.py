@@ -14,8 +14,10 @@ from .api import (  # noqa: F401
     buildF,
     buildG,
     buildH,
+    evaluate,
     initial_factors,
     make_opts,
+    quality_ybz,
     soft_threshold,
     triple_decomp_ADMM,
     triple_decomp_ADMM_outlier,

@@ -87,6 +87,10 @@ SIGNATURES = {
     "tritd_als_session_destroy": (None, [vp]),
     "tritd_als_sharded_virtual_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp,
                                                 i32, vp, vp, vp, vp, C.POINTER(i32), i32]),
+    "tritd_evaluate_f64": (C.c_int, [vp, i64, vp, i64, vp, dp, dp]),
+    "tritd_quality_f64": (C.c_int, [vp, vp, i64, i64, i64, dp, dp, vp, vp]),
+    "tritd_dev_evaluate_f64": (C.c_int, [vp, i64, vp, i64, vp, dp, dp, vp]),
+    "tritd_dev_quality_f64": (C.c_int, [vp, vp, i64, i64, i64, dp, dp, vp, vp, vp]),
     "tritd_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp]),
     "tritd_unfold_f64": (C.c_int, [vp, i64, i64, i64, i32, vp]),
     "tritd_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp]),

@@ -10,6 +10,8 @@ the MATLAB file it replaces and runs on the GPU through libtritd.so:
     unfold(X, mode)                         unfold.m:1
     soft_threshold(X, lam)                  soft_threshold.m:1
     buildF(B, C) / buildG(A, C) / buildH(A, B)   buildF.m:1 / buildG.m:1 / buildH.m:1
+    evaluate(X, gt, mask)                   traffic_triple_comparison.m:194-202
+    quality_ybz(X1, X2)                     other_methods/Low-rank-.../quality_ybz.m:1
 
 Arrays are numpy, MATLAB (column-major) semantics.  `opts` is a dict (or any
 object with attributes) holding the fields the reference reads
@@ -250,6 +252,44 @@ def soft_threshold(X, lam):
     return Y
 
 
+def evaluate(X, gt, mask=None):
+    """[rmse, nrmse] = evaluate(X, gt, mask)  (traffic_triple_comparison.m:194-202):
+    rmse = norm(X(mask) - gt(:)), nrmse = rmse / norm(gt(:)); mask None means
+    true(size(X)).  gt holds the masked entries in column-major order."""
+    X = _fortran(X)
+    gt = _fortran(gt)
+    m = None
+    if mask is not None:
+        mk = np.asarray(mask)
+        if mk.shape != X.shape:
+            raise ValueError("Index exceeds the number of array elements (mask shape differs).")
+        m = np.asfortranarray(mk != 0).view(np.uint8)
+    rmse, nrmse = C.c_double(0), C.c_double(0)
+    check(lib.tritd_evaluate_f64(_ptr(X), X.size, _ptr(gt), gt.size, _ptr(m) if m is not None else None,
+                                 C.byref(rmse), C.byref(nrmse)))
+    return rmse.value, nrmse.value
+
+
+def quality_ybz(imagery1, imagery2, per_frame=False):
+    """[psnr, ssim] = quality_ybz(imagery1, imagery2): mean over the frames
+    (dims 3.. folded) of psnr_index and ssim_index (dynamic range [0, 255])."""
+    X1 = _fortran(imagery1)
+    X2 = _fortran(imagery2)
+    if X1.shape != X2.shape:
+        raise ValueError("imagery1 and imagery2 must have the same size")
+    n1 = X1.shape[0]
+    n2 = X1.shape[1] if X1.ndim > 1 else 1
+    nf = max(X1.size // max(n1 * n2, 1), 1)
+    p, s = C.c_double(0), C.c_double(0)
+    pf = np.zeros(nf)
+    sf = np.zeros(nf)
+    check(lib.tritd_quality_f64(_ptr(X1), _ptr(X2), n1, n2, nf, C.byref(p), C.byref(s), _ptr(pf),
+                                _ptr(sf)))
+    if per_frame:
+        return p.value, s.value, pf, sf
+    return p.value, s.value
+
+
 def _design(which, P, Q, nP, nQ, r):
     out = np.zeros((r * r, nP * nQ), order="F")
     check(lib.tritd_build_design_f64(which.encode(), _ptr(P), _ptr(Q), nP, nQ, r, _ptr(out)))
@@ -467,6 +507,6 @@ class Comm:
 
 
 __all__ = ["triple_decomp_ADMM", "triple_decomp_ADMM_outlier", "triple_decomp_ALS", "AlsSession",
-           "make_als_opts", "triple_product", "unfold",
+           "make_als_opts", "evaluate", "quality_ybz", "triple_product", "unfold",
            "soft_threshold", "buildF", "buildG", "buildH", "Session", "Comm", "TritdError",
            "make_opts", "initial_factors"]
