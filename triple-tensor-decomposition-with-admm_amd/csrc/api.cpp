@@ -715,37 +715,25 @@ tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, cons
                                           int64_t n1, int64_t n2, int64_t n3, int32_t r, double* X,
                                           void* stream) {
     return guarded([&] {
-        check_dims(n1, n2, n3, r);
+        check_dims(n1, n2, n3, r, true);
         need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
         hipStream_t st = as_stream(stream);
-        const Geom g = make_geom(n1, n2, n3, 0, n1, r);
-        const int64_t R = (int64_t)r * r;
-        std::vector<double> hA(n1 * R), hB(R * n2), hC(R * n3);
-        TRITD_HIP(hipMemcpyAsync(hA.data(), A, hA.size() * 8, hipMemcpyDeviceToHost, st));
-        TRITD_HIP(hipMemcpyAsync(hB.data(), B, hB.size() * 8, hipMemcpyDeviceToHost, st));
-        TRITD_HIP(hipMemcpyAsync(hC.data(), C, hC.size() * 8, hipMemcpyDeviceToHost, st));
-        TRITD_HIP(hipStreamSynchronize(st));
-        std::vector<double> Ah, AhT, Bh, Ch, ChT;
-        pack_A(g, hA.data(), Ah, AhT);
-        pack_B(g, hB.data(), Bh);
-        pack_C(g, hC.data(), Ch, ChT);
-        DBuf dAh, dBh, dChT, L;
-        dAh.alloc(Ah.size()); dBh.alloc(Bh.size()); dChT.alloc(ChT.size());
-        TRITD_HIP(hipMemcpy(dAh.p, Ah.data(), Ah.size() * 8, hipMemcpyHostToDevice));
-        TRITD_HIP(hipMemcpy(dBh.p, Bh.data(), Bh.size() * 8, hipMemcpyHostToDevice));
-        TRITD_HIP(hipMemcpy(dChT.p, ChT.data(), ChT.size() * 8, hipMemcpyHostToDevice));
-        L.alloc((size_t)g.Np);
-        launch_tp(g, dAh.p, dBh.p, dChT.p, L.p, nullptr, nullptr, 0, st);
-        TRITD_HIP(hipMemcpy2DAsync(X, n1 * 8, L.p, g.n1p * 8, n1 * 8, (size_t)(n2 * n3),
-                                   hipMemcpyDeviceToDevice, st));
-        TRITD_HIP(hipStreamSynchronize(st));
+        Geom g = make_geom(n1, n2, n3, 0, n1, r);
+        g.RP = padded_rank32(g.R);  // 16..256: the kernel is instantiated for every padded rank
+        DBuf Ah, Bh, ChT;
+        Ah.alloc((size_t)(g.n1p * g.RP));
+        Bh.alloc((size_t)(n2 * g.RP));
+        ChT.alloc((size_t)g.RP * g.n3p);
+        launch_pack_factors(g, A, B, C, Ah.p, Bh.p, ChT.p, st);
+        launch_tp(g, Ah.p, Bh.p, ChT.p, X, nullptr, nullptr, 0, n1, n1 * n2, st);
+        TRITD_HIP(hipStreamSynchronize(st));  // the factor copies are freed on return
     });
 }
 
 tritd_status tritd_triple_product_f64(const double* A, const double* B, const double* C, int64_t n1,
                                       int64_t n2, int64_t n3, int32_t r, double* X) {
     return guarded([&] {
-        check_dims(n1, n2, n3, r);
+        check_dims(n1, n2, n3, r, true);  // r <= 16
         need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
         pick_device(-1);
         const int64_t R = (int64_t)r * r;

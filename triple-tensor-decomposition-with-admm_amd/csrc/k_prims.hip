@@ -42,42 +42,68 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 }
 
 // ---------------------------------------------------------------------------
-// triple product L(i,j,t) = sum_k Ah(i,k) Bh(j,k) Ch(t,k) in the padded layout.
+// triple product L(i,j,t) = sum_k Ah(i,k) Bh(j,k) Ch(t,k)  (triple_product.m:6)
+// written to / compared against a strided tensor X(i,j,t) = X[i + ldj*j + ldt*t]
+// (the caller's column-major array: ldj = n1, ldt = n1*n2; no padded copy).
 // mode 0: write L; mode 1: per-block partials of sum (L-X)^2 and sum X^2
 // (the driver's RRE, traffic_triple_comparison.m:62-63,194-199).
+// A wave owns one ij-tile (16 rows i of one fibre j, KR row in registers);
+// the block stages C^T for TPC t-values at a time in LDS and every wave runs
+// two independent MFMA chains (two t-tiles) per step.  Bound: f64 MFMA
+// (2*N*R flops) for RP >= 32, the N*8 B write below.
 // ---------------------------------------------------------------------------
+constexpr int TP_WAVES = 8;
+constexpr int TPC = 32;  // t-values per LDS chunk (two t-tiles)
+
 template <int RP, int MODE>
-__global__ __launch_bounds__(512) void k_tp(const double* __restrict__ Ah,
-                                            const double* __restrict__ Bh,
-                                            const double* __restrict__ ChT, double* L,
-                                            const double* __restrict__ X, double* partial,
-                                            int64_t n1p, int64_t n3p, int64_t plane, int64_t tiles) {
+__global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__ Ah,
+                                                      const double* __restrict__ Bh,
+                                                      const double* __restrict__ ChT, double* L,
+                                                      const double* __restrict__ X, double* partial,
+                                                      int64_t n1p, int64_t n1l, int64_t n3,
+                                                      int64_t n3p, int64_t tiles, int64_t ldj,
+                                                      int64_t ldt) {
     constexpr int KS = RP / 4;
+    constexpr int LDT = TPC + 16;  // 2*LDT = 96 = 32 mod 64 dwords: no bank conflicts per half-wave
+    __shared__ double cs[RP * LDT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int il = lane & 15, tg = lane >> 4;
-    const int64_t tile = (int64_t)blockIdx.x * 8 + wid;
+    const int64_t tile = (int64_t)blockIdx.x * TP_WAVES + wid;
     const bool active = tile < tiles;
     const int64_t qper = n1p >> 4;
     const int64_t j = active ? tile / qper : 0;
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
-    const int64_t base = (tile << 4) + il;
+    const bool row_ok = active && i < n1l;
     double kr[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
         const int k = 4 * s + tg;
         kr[s] = active ? Ah[i * RP + k] * Bh[j * RP + k] : 0.0;
     }
+    const int64_t obase = i + ldj * j;
     double sn = 0.0, sd = 0.0;
-    if (active) {
-        for (int64_t t0 = 0; t0 < n3p; t0 += 16) {
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t c0 = 0; c0 < n3p; c0 += TPC) {
+        __syncthreads();  // the previous chunk is consumed
+        for (int e = threadIdx.x; e < RP * TPC; e += 64 * TP_WAVES) {
+            const int k = e / TPC, t = e % TPC;
+            cs[k * LDT + t] = (c0 + t < n3p) ? ChT[(int64_t)k * n3p + c0 + t] : 0.0;
+        }
+        __syncthreads();
+        d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ChT[(int64_t)(4 * s + tg) * n3p + t0 + il],
-                                                           kr[s], acc, 0, 0, 0);
+        for (int s = 0; s < KS; ++s) {
+            const double* row = cs + (4 * s + tg) * LDT + il;
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[0], kr[s], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16], kr[s], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const d4 acc = h ? acc1 : acc0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int64_t off = (t0 + tg + 4 * r) * plane + base;
+                const int64_t t = c0 + 16 * h + tg + 4 * r;
+                if (!row_ok || t >= n3) continue;
+                const int64_t off = obase + ldt * t;
                 if (MODE == 0) {
                     L[off] = acc[r];
                 } else {
@@ -95,7 +121,7 @@ __global__ __launch_bounds__(512) void k_tp(const double* __restrict__ Ah,
             sn += __shfl_xor(sn, off);
             sd += __shfl_xor(sd, off);
         }
-        __shared__ double red[2][8];
+        __shared__ double red[2][TP_WAVES];
         if (lane == 0) {
             red[0][wid] = sn;
             red[1][wid] = sd;
@@ -103,7 +129,7 @@ __global__ __launch_bounds__(512) void k_tp(const double* __restrict__ Ah,
         __syncthreads();
         if (threadIdx.x == 0) {
             double a = 0.0, b = 0.0;
-            for (int w = 0; w < 8; ++w) {
+            for (int w = 0; w < TP_WAVES; ++w) {
                 a += red[0][w];
                 b += red[1][w];
             }
@@ -113,19 +139,20 @@ __global__ __launch_bounds__(512) void k_tp(const double* __restrict__ Ah,
     }
 }
 
-int tp_grid(const Geom& g) { return (int)cdiv(g.tiles, 8); }
+int tp_grid(const Geom& g) { return (int)cdiv(g.tiles, TP_WAVES); }
 
 void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
-               const double* X, double* partial, int mode, hipStream_t st) {
-    const dim3 grid(tp_grid(g)), block(512);
+               const double* X, double* partial, int mode, int64_t ldj, int64_t ldt,
+               hipStream_t st) {
+    const dim3 grid(tp_grid(g)), block(64 * TP_WAVES);
 #define TP_CASE(RPV)                                                                            \
     case RPV:                                                                                   \
         if (mode == 0)                                                                          \
             hipLaunchKernelGGL((k_tp<RPV, 0>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
-                               g.n1p, g.n3p, g.plane, g.tiles);                                 \
+                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt);                  \
         else                                                                                    \
             hipLaunchKernelGGL((k_tp<RPV, 1>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
-                               g.n1p, g.n3p, g.plane, g.tiles);                                 \
+                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt);                  \
         break;
     switch (g.RP) {
         TP_CASE(16)
@@ -138,6 +165,45 @@ void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* 
             throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by triple_product");
     }
 #undef TP_CASE
+    TRITD_CHECK_LAUNCH();
+}
+
+// Reference-layout factors (device) -> the CP factor layout of common.h:
+// Ah[i*RP+k] = A(i,p,q), Bh[j*RP+k] = B(p,j,q), ChT[k*n3p+t] = C(p,q,t),
+// k = p + r*q (zero for k >= R and for the padded rows)
+__global__ __launch_bounds__(256) void k_pack_factors(const double* __restrict__ A,
+                                                      const double* __restrict__ B,
+                                                      const double* __restrict__ C, int64_t n1,
+                                                      int64_t n2, int64_t n3, int r, int RP,
+                                                      int64_t n1p, int64_t n3p, double* Ah,
+                                                      double* Bh, double* ChT) {
+    const int R = r * r;
+    const int64_t na = n1p * RP, nb = n2 * RP, nc = (int64_t)RP * n3p;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < na + nb + nc;
+         e += (int64_t)gridDim.x * 256) {
+        if (e < na) {
+            const int64_t i = e / RP;
+            const int k = (int)(e % RP);
+            Ah[e] = (i < n1 && k < R) ? A[i + n1 * k] : 0.0;
+        } else if (e < na + nb) {
+            const int64_t f = e - na, jj = f / RP;
+            const int k = (int)(f % RP), p = k % r, q = k / r;
+            Bh[f] = k < R ? B[p + (int64_t)r * jj + (int64_t)r * n2 * q] : 0.0;
+        } else {
+            const int64_t f = e - na - nb, t = f % n3p;
+            const int k = (int)(f / n3p);
+            ChT[f] = (k < R && t < n3) ? C[k + (int64_t)R * t] : 0.0;
+        }
+    }
+}
+
+void launch_pack_factors(const Geom& g, const double* A, const double* B, const double* C,
+                         double* Ah, double* Bh, double* ChT, hipStream_t st) {
+    const int64_t tot = g.n1p * g.RP + g.n2 * g.RP + (int64_t)g.RP * g.n3p;
+    int64_t b = cdiv(tot, 256);
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(k_pack_factors, dim3((unsigned)b), dim3(256), 0, st, A, B, C, g.n1, g.n2,
+                       g.n3, g.r, g.RP, g.n1p, g.n3p, Ah, Bh, ChT);
     TRITD_CHECK_LAUNCH();
 }
 

@@ -79,11 +79,17 @@ void launch_vsum(double* const* bufs, int nbufs, int64_t count, hipStream_t st);
 void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nblocks,
                          hipStream_t st);
 int sumsq_blocks(const Geom& g);
-// triple product of device factors into the padded layout (mode 0) or the
-// RRE partial sums against X (mode 1: partial[2*b] = sum (L-X)^2, [2*b+1] = sum X^2)
+// triple product of device factors (layout of common.h) into / against a
+// strided tensor X(i,j,t) = X[i + ldj*j + ldt*t] of the shard's n1l x n2 x n3:
+// mode 0 writes L; mode 1 writes RRE partials partial[2*b] = sum (L-X)^2,
+// [2*b+1] = sum X^2 (traffic_triple_comparison.m:62-63,194-199)
 int tp_grid(const Geom& g);
 void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
-               const double* X, double* partial, int mode, hipStream_t st);
+               const double* X, double* partial, int mode, int64_t ldj, int64_t ldt,
+               hipStream_t st);
+// reference-layout device factors A (n1,r,r), B (r,n2,r), C (r,r,n3) -> Ah, Bh, ChT
+void launch_pack_factors(const Geom& g, const double* A, const double* B, const double* C,
+                         double* Ah, double* Bh, double* ChT, hipStream_t st);
 void launch_transpose_batched(const double* in, double* out, int64_t rows, int64_t cols,
                               int64_t batch, hipStream_t st);
 // layout conversions of the big tensors: column-major shard (leading dim ld,

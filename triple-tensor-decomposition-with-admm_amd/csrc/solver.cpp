@@ -746,9 +746,7 @@ void Session::counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch) {
 
 void Session::rre_parts(const void* dX, int64_t ldX, double* num, double* den) {
     TRITD_HIP(hipSetDevice(device_));
-    DBuf Xp, Xd, part, out;
-    Xp.alloc((size_t)g_.Np);
-    TRITD_HIP(hipMemsetAsync(Xp.p, 0, Xp.n * sizeof(double), st_));
+    DBuf Xd, part, out;
     const double* src = static_cast<const double*>(dX);
     if (f32_) {  // the reference tensor in single: widen (exactly) to double
         const int64_t cnt = (g_.n2 * g_.n3 - 1) * ldX + g_.n1l;
@@ -756,13 +754,11 @@ void Session::rre_parts(const void* dX, int64_t ldX, double* num, double* den) {
         launch_widen(static_cast<const float*>(dX), cnt, Xd.p, st_);
         src = Xd.p;
     }
-    TRITD_HIP(hipMemcpy2DAsync(Xp.p, g_.n1p * sizeof(double), src, ldX * sizeof(double),
-                               g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
-                               hipMemcpyDeviceToDevice, st_));
     const int grid = tp_grid(g_);
     part.alloc(2 * (size_t)grid);
     out.alloc(2);
-    launch_tp(g_, Ah_.p, Bh_.p, ChT_.p, nullptr, Xp.p, part.p, 1, st_);
+    // X(i,j,t) of the shard at src[i + ldX*(j + n2*t)]
+    launch_tp(g_, Ah_.p, Bh_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_);
     launch_reduce_pairs(part.p, grid, out.p, nullptr, st_);
     double h[2];
     TRITD_HIP(hipMemcpyAsync(h, out.p, sizeof h, hipMemcpyDeviceToHost, st_));
