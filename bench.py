@@ -179,17 +179,19 @@ def main():
     errhist_final = float(res["errHist"][-1]) if len(res["errHist"]) else None
 
     # algorithmic bytes of the dominant kernel (fused update K5), per launch,
-    # on this rank's shard: reads D, Y_L, Y_O + writes Y_L, Y_O,
-    # T (6 N-streams of s bytes; O is rebuilt on demand), E in compact form
-    # (one 256 B slot per 256-element tile read and written), a whole tile
-    # (256 * s bytes) for each tile stored densely (read next launch), and W
-    # (R * n_local * n2 elements)
+    # on this rank's shard: `streams` dense N-streams of s bytes
+    # (fp64: D, Y_L read + Y_L, T written, Y_O rebuilt from Y_L and E; fp32:
+    # D, Y_L, Y_O read + Y_L, Y_O, T written; O is rebuilt on demand), E in
+    # compact form (`slots` 256 B slot accesses per 256-element tile: E^(k) and
+    # E^(k-1) read + E^(k+1) written, or E read + written), whole tiles
+    # (256 * s bytes) for the tiles stored densely, and W (R * n_local * n2 elements)
     s_b = 4 if f32 else 8
     nl = i1 - i0
     N_local = nl * n2 * n3
     tile_b = 256 * s_b
-    k5_bytes = int(6 * N_local * s_b + 2 * tiles_per_launch * 256 + dense_per_launch * tile_b
-                   + r * r * nl * n2 * s_b)
+    streams, slots = sess.k5_profile()
+    k5_bytes = int(streams * N_local * s_b + slots * tiles_per_launch * 256
+                   + (slots - 1) * dense_per_launch * tile_b + r * r * nl * n2 * s_b)
     # flops: L(ij,t) = sum_k (Ah*Bh)(ij,k) Ch(t,k) and W = T x3 Ch, 2 N R each
     k5_flops = 4.0 * N_local * r * r
     k5_ms = km["fused_update"]
@@ -206,6 +208,7 @@ def main():
                 "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
                 "mfma_achieved_TFs": tfs}
     roof.update({"kernel": "k5_fused (fused ADMM update + L + W)", "traffic": traffic,
+                 "dense_streams": streams, "slot_accesses_per_tile": slots,
                  "traffic_source": traffic_src, "algorithmic_bytes_per_launch": k5_bytes,
                  "e_dense_tiles_per_launch": dense_per_launch,
                  "e_tiles_per_launch": tiles_per_launch})

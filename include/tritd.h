@@ -162,6 +162,12 @@ tritd_status tritd_session_probe(tritd_session* s, double* ms, int32_t cap, int3
  * number of tiles one launch covers. */
 tritd_status tritd_session_counters(tritd_session* s, int64_t* dense_tiles_total,
                                     int64_t* tiles_per_launch);
+/* Streaming profile of the session's fused update: dense
+ * N-element streams per launch (6 = D, Y_L, Y_O read + Y_L, Y_O, T written;
+ * 4 with the derived Y_O of the fp64 path) and compact-E slot accesses per
+ * tile (2 = E read + written; 3 = E^(k), E^(k-1) read + E^(k+1) written). */
+tritd_status tritd_session_k5_profile(tritd_session* s, int32_t* dense_streams,
+                                      int32_t* slot_accesses);
 void tritd_session_destroy(tritd_session* s);
 
 /* ---------------------------------------------------------------------------

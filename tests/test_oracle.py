@@ -273,3 +273,19 @@ def test_oracle_evaluate_masked_order():
     rmse, nrmse = orc.evaluate(Xh.ravel(order="F")[mask.ravel(order="F")], gt)
     assert abs(rmse - np.linalg.norm((Xh - X)[mask])) < 1e-14
     assert abs(nrmse - rmse / np.linalg.norm(X[mask])) < 1e-14
+
+
+def test_derived_yo_identity_in_the_restatement():
+    """The identity K5's derived-Y_O mode relies on (k_admm.hip header):
+    with muL == muO (:16-17), Y_L^(k) - Y_O^(k) = mu_k (E^(k) - E^(k-1)) for
+    every k, up to rounding — checked on the restatement's own trace."""
+    g = load_golden("g12x10x8_r2")
+    *_, tr = orc.triple_decomp_ADMM(g["D"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                    trace_iters=(1, 2, 3, 7))
+    mus = orc.mu_schedule(g["opts"]["mu"], g["opts"]["rho"], 10)
+    E_prev = {1: np.zeros_like(tr[1]["E"]), 2: tr[1]["E"], 3: tr[2]["E"]}
+    for k in (1, 2, 3):
+        lhs = tr[k]["Y_L"] - tr[k]["Y_O"]
+        rhs = mus[k - 1] * (tr[k]["E"] - E_prev[k])
+        scale = np.abs(tr[k]["Y_L"]).max()
+        assert np.abs(lhs - rhs).max() <= 1e-13 * scale, k

@@ -517,6 +517,17 @@ tritd_status tritd_session_counters(tritd_session* s, int64_t* dense_tiles_total
     });
 }
 
+tritd_status tritd_session_k5_profile(tritd_session* s, int32_t* dense_streams,
+                                      int32_t* slot_accesses) {
+    return guarded([&] {
+        need(s, "session"); need(dense_streams, "dense_streams"); need(slot_accesses, "slot_accesses");
+        int a = 0, b = 0;
+        reinterpret_cast<Session*>(s)->k5_profile(&a, &b);
+        *dense_streams = a;
+        *slot_accesses = b;
+    });
+}
+
 void tritd_session_destroy(tritd_session* s) { delete reinterpret_cast<Session*>(s); }
 
 tritd_status tritd_comm_unique_id(void* id128) {

@@ -27,6 +27,17 @@
 // W^T accumulates in registers over the whole t range, so W leaves the chip
 // once.
 //
+// Derived Y_O (DY, the default for fp64): with muL == muO (both are opts.mu,
+// :16-17, and follow one schedule, :56-57), :43 gives 2 O = (D - L) + E^(k-1)
+// + (Y_L - Y_O)/mu, hence from :51-53
+//   Y_L^(k) - Y_O^(k) = (Y_L - Y_O) + mu (D - L - 2 O + E^(k)) = mu_k (E^(k) - E^(k-1))
+// exactly, for every k (Y_L^(0) = Y_O^(0) = 0).  So Y_O is never stored: the
+// K5 of iteration k+1 reads Y_L^(k) and the compact E^(k), E^(k-1) (256 B per
+// tile each) and forms Y_O^(k) = Y_L^(k) - mu_k (E^(k) - E^(k-1)) — 4 dense
+// N-streams instead of 6.  The rebuilt Y_O differs from MATLAB's by rounding
+// only (checked against the restatement on every golden case: L, O, E within
+// 1e-11, same k; tests/test_gpu_parity.py holds the GPU to 1e-9).
+//
 // Elementwise arithmetic follows MATLAB's expression order exactly; the file
 // is compiled with -ffp-contract=off so no statement is fused into an FMA.
 #include "kernels.h"
@@ -166,7 +177,7 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
 
 // Two waves per SIMD (VGPRs + AGPRs <= 256): at one wave per SIMD the
 // streams do not keep enough bytes in flight (measured +6 % K5 time).
-template <int RP, bool PRO>
+template <int RP, bool PRO, bool DY>
 __global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k5_fused(K5Args a) {
     if (*a.stop) return;
@@ -249,6 +260,9 @@ void k5_fused(K5Args a) {
     const d2v* D2 = reinterpret_cast<const d2v*>(a.D);
     d2v* O2 = reinterpret_cast<d2v*>(a.O);
     d2v* E2 = reinterpret_cast<d2v*>(a.E);
+    d2v* Ep2 = reinterpret_cast<d2v*>(a.Ep);     // DY: E^(k-1) dense tiles, E^(k+1) destination
+    d2v* Eout2 = DY ? Ep2 : E2;
+    double* CEout = DY ? a.CEp : a.CE;
     d2v* YL2 = reinterpret_cast<d2v*>(a.YL);
     d2v* YO2 = reinterpret_cast<d2v*>(a.YO);
     d2v* T2 = reinterpret_cast<d2v*>(a.T);
@@ -265,10 +279,13 @@ void k5_fused(K5Args a) {
     // makes the compiler's in-order vmcnt waits conservative, i.e. it waits
     // on the batch it just issued).  Nothing depends on `active` either (a
     // wave past the last tile streams the zero-filled group padding).
+    // DY: x[2] is unused (Y_O is rebuilt); edp/cep hold E^(k-1) like ed/ce
     struct Regs {
         d2v x[3][2];
         d2v ed[2];
         double ce;
+        d2v edp[2];
+        double cep;
     };
     __shared__ double csm[K5_WAVES][96];
     double* cs = csm[wid];
@@ -278,7 +295,7 @@ void k5_fused(K5Args a) {
         for (int p = 0; p < 2; ++p) {
             nx.x[0][p] = ld2(D2 + o + 64 * p);
             nx.x[1][p] = ld2(YL2 + o + 64 * p);
-            nx.x[2][p] = ld2((PRO ? O2 : YO2) + o + 64 * p);
+            if (PRO || !DY) nx.x[2][p] = ld2((PRO ? O2 : YO2) + o + 64 * p);
         }
     };
     auto load_dense = [&](int64_t tt, Regs& nx) {
@@ -286,9 +303,16 @@ void k5_fused(K5Args a) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) nx.ed[p] = E2[o + 64 * p];
     };
-    auto load_slot = [&](int64_t tt, double& ce) {
+    auto load_dense_p = [&](int64_t tt, Regs& nx) {
+        const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) nx.edp[p] = Ep2[o + 64 * p];
+    };
+    auto load_slot = [&](int64_t tt, Regs& rx) {
         const int64_t t2 = tt < ntt ? tt : ntt - 1;  // clamped: no branch
-        ce = a.CE[(tm_tile_base(tile, phys(t2), ntt) >> 8) * CE_SLOT + (lane & 31)];
+        const int64_t so = (tm_tile_base(tile, phys(t2), ntt) >> 8) * CE_SLOT + (lane & 31);
+        rx.ce = a.CE[so];
+        if (DY) rx.cep = a.CEp[so];
     };
     // one t-tile: cx holds its data; if `pf`, tile tt+1 is prefetched into nx
     // and its C^ slice staged into buffer buf^1
@@ -299,6 +323,7 @@ void k5_fused(K5Args a) {
         // arrived with the batch of this tile
         if (pf) {
             const bool dn1 = PRO ? false : ce_is_dense(nx.ce);
+            const bool dnp1 = (PRO || !DY) ? false : ce_is_dense(nx.cep);
             stage_load(tt + 1);
             load(tt + 1, nx);
             // keep the prefetch ahead of the compute: the scheduler otherwise
@@ -309,15 +334,23 @@ void k5_fused(K5Args a) {
             // the batch and consumed a step later, so the common path's waits
             // stay exact
             if (!PRO && dn1) load_dense(tt + 1, nx);
+            if (!PRO && DY && dnp1) load_dense_p(tt + 1, nx);
         }
-        double ev[4];
+        double ev[4], evp[4];
         if (!PRO) {
             const bool dn = ce_decode(cx.ce, lane, ev);
             ev[0] = dn ? cx.ed[0][0] : ev[0];
             ev[1] = dn ? cx.ed[0][1] : ev[1];
             ev[2] = dn ? cx.ed[1][0] : ev[2];
             ev[3] = dn ? cx.ed[1][1] : ev[3];
-            if (pf) load_slot(tt + 2, cx.ce);  // cx.ce was consumed above
+            if (DY) {
+                const bool dp = ce_decode(cx.cep, lane, evp);
+                evp[0] = dp ? cx.edp[0][0] : evp[0];
+                evp[1] = dp ? cx.edp[0][1] : evp[1];
+                evp[2] = dp ? cx.edp[1][0] : evp[2];
+                evp[3] = dp ? cx.edp[1][1] : evp[3];
+            }
+            if (pf) load_slot(tt + 2, cx);  // cx.ce (and cx.cep) were consumed above
         }
         const double* cT = sCT[buf];
         const double* cR = sC[buf];
@@ -344,8 +377,9 @@ void k5_fused(K5Args a) {
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     const int r = 2 * p + q;
-                    const double d = cx.x[0][p][q], yl = cx.x[1][p][q], e = ev[r],
-                                 yo = cx.x[2][p][q];
+                    const double d = cx.x[0][p][q], yl = cx.x[1][p][q], e = ev[r];
+                    // DY: Y_O^(k) = Y_L^(k) - muO_k (E^(k) - E^(k-1))  (header)
+                    const double yo = DY ? yl - sc.muO_prev * (e - evp[r]) : cx.x[2][p][q];
                     const double L = lacc[r];
                     const double R1 = (d - L) + sc.invL * yl;               // :41
                     const double R2 = e - sc.invO * yo;                     // :42
@@ -365,9 +399,9 @@ void k5_fused(K5Args a) {
                     tr[r] = Tn;
                 }
                 st2(YLn2, YL2 + o + 64 * p);
-                st2(YOn2, YO2 + o + 64 * p);
+                if (!DY) st2(YOn2, YO2 + o + 64 * p);
             }
-            ce_encode(En, lane, cs, a.CE, (tb >> 8) * CE_SLOT, E2, o, ndense);
+            ce_encode(En, lane, cs, CEout, (tb >> 8) * CE_SLOT, Eout2, o, ndense);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
         if (K5_EXP & 8) {
@@ -408,13 +442,15 @@ void k5_fused(K5Args a) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) xa.x[q][0] = xa.x[q][1] = xb.x[q][0] = xb.x[q][1] = d2v{0.0, 0.0};
     xa.ed[0] = xa.ed[1] = xb.ed[0] = xb.ed[1] = d2v{0.0, 0.0};
-    xa.ce = xb.ce = 0.0;
+    xa.edp[0] = xa.edp[1] = xb.edp[0] = xb.edp[1] = d2v{0.0, 0.0};
+    xa.ce = xb.ce = xa.cep = xb.cep = 0.0;
     if (!PRO) {
-        load_slot(0, xa.ce);
-        load_slot(1, xb.ce);
+        load_slot(0, xa);
+        load_slot(1, xb);
     }
     load(0, xa);
     if (!PRO && ce_is_dense(xa.ce)) load_dense(0, xa);
+    if (!PRO && DY && ce_is_dense(xa.cep)) load_dense_p(0, xa);
     stage(0, 0);
     __syncthreads();
     int64_t tt = 0;
@@ -468,14 +504,16 @@ void k5_fused(K5Args a) {
 
 int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }
 
-void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st) {
+void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st) {
     const dim3 grid(k5_grid(g)), block(64 * K5_WAVES);
-#define K5_CASE(RPV)                                                           \
-    case RPV:                                                                  \
-        if (prologue)                                                          \
-            hipLaunchKernelGGL((k5_fused<RPV, true>), grid, block, 0, st, a);  \
-        else                                                                   \
-            hipLaunchKernelGGL((k5_fused<RPV, false>), grid, block, 0, st, a); \
+#define K5_CASE(RPV)                                                                 \
+    case RPV:                                                                        \
+        if (prologue)                                                                \
+            hipLaunchKernelGGL((k5_fused<RPV, true, false>), grid, block, 0, st, a); \
+        else if (dy)                                                                 \
+            hipLaunchKernelGGL((k5_fused<RPV, false, true>), grid, block, 0, st, a); \
+        else                                                                         \
+            hipLaunchKernelGGL((k5_fused<RPV, false, false>), grid, block, 0, st, a); \
         break;
     switch (g.RP) {
         K5_CASE(16)
@@ -616,13 +654,13 @@ void launch_o_fixup(const Geom& g, const double* D, const double* YL, const doub
     TRITD_CHECK_LAUNCH();
 }
 
-// Placement probe: K5's HBM pattern (read D, Y_L, Y_O and the tile's 256 B
-// compact-E slot; write Y_L, Y_O in place, T and the slot; one wave per
-// ij-tile walking its t-tiles, prefetched) without the arithmetic.  K5 is
-// HBM-bound (dropping all its compute leaves its time unchanged) and its
-// bandwidth depends on where the pool landed physically; the session times
-// candidate pools with this and keeps the fastest.  Contents
-// are overwritten with garbage.
+// Placement probe: K5's HBM pattern (read D, Y_L, Y_O (not with dy) and the
+// tile's 256 B compact-E slot; write Y_L, Y_O (not with dy) in place, T and
+// the slot; one wave per ij-tile walking its t-tiles, prefetched) without the
+// arithmetic.  K5 is HBM-bound and its bandwidth depends on where the pool
+// landed physically; the session times candidate pools with this and keeps
+// the fastest.  Contents are overwritten with garbage.
+template <bool DY>
 __global__ __launch_bounds__(256) void k_pool_probe(double* D, double* YL, double* YO, double* T,
                                                     double* CE, int64_t tiles4, int64_t ntt) {
     const int lane = threadIdx.x & 63;
@@ -641,7 +679,7 @@ __global__ __launch_bounds__(256) void k_pool_probe(double* D, double* YL, doubl
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int f = 0; f < 3; ++f) nx.x[f][p] = P[f][o + 64 * p];
+            for (int f = 0; f < (DY ? 2 : 3); ++f) nx.x[f][p] = P[f][o + 64 * p];
         nx.ce = CE[(tb(tt) >> 8) * CE_SLOT + (lane & 31)];
     };
     auto body = [&](int64_t tt, R& c, R& n, bool pf) {
@@ -652,9 +690,14 @@ __global__ __launch_bounds__(256) void k_pool_probe(double* D, double* YL, doubl
         const int64_t o = (tb(tt) >> 1) + lane;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            P[1][o + 64 * p] = c.x[0][p] + c.x[1][p];
-            P[2][o + 64 * p] = c.x[2][p] - c.x[1][p];
-            P[3][o + 64 * p] = c.x[0][p] - c.x[2][p];
+            if (DY) {
+                P[1][o + 64 * p] = c.x[0][p] + c.x[1][p];
+                P[3][o + 64 * p] = c.x[0][p] - c.x[1][p];
+            } else {
+                P[1][o + 64 * p] = c.x[0][p] + c.x[1][p];
+                P[2][o + 64 * p] = c.x[2][p] - c.x[1][p];
+                P[3][o + 64 * p] = c.x[0][p] - c.x[2][p];
+            }
         }
         CE[(tb(tt) >> 8) * CE_SLOT + (lane & 31)] = c.ce + 1.0;
     };
@@ -673,9 +716,13 @@ __global__ __launch_bounds__(256) void k_pool_probe(double* D, double* YL, doubl
 }
 
 void launch_pool_probe(const Geom& g, double* D, double* YL, double* YO, double* T, double* CE,
-                       hipStream_t st) {
-    hipLaunchKernelGGL(k_pool_probe, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D, YL, YO, T,
-                       CE, g.tiles4, g.ntt);
+                       bool dy, hipStream_t st) {
+    if (dy)
+        hipLaunchKernelGGL(k_pool_probe<true>, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D,
+                           YL, YO, T, CE, g.tiles4, g.ntt);
+    else
+        hipLaunchKernelGGL(k_pool_probe<false>, dim3((unsigned)(g.tiles4 / 4)), dim3(256), 0, st, D,
+                           YL, YO, T, CE, g.tiles4, g.ntt);
     TRITD_CHECK_LAUNCH();
 }
 

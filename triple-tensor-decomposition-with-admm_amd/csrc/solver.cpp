@@ -89,6 +89,8 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         if (ovmode_ == 0) overlap_ = false;
         // one process per GPU with a communicator: the sharded schedule with
         // its off-critical-path Grams and solves on the side stream
+        const char* dy = std::getenv("TRITD_DY");
+        dy_ = !f32_ && !(dy && std::atoi(dy) == 0);
         const char* sh = std::getenv("TRITD_SHOV");
         shov_ = comm != nullptr && comm->comm != nullptr && shared_stream == nullptr &&
                 !(sh && std::atoi(sh) == 0);
@@ -124,8 +126,10 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         const size_t pool_bytes = 6 * slot;
         // compact E: 256 B per tile in either data type (before probing: the probe streams it)
         CE_.alloc_bytes((size_t)(g_.Ntm / 256) * 256);
+        if (dy_) CE2_.alloc_bytes((size_t)(g_.Ntm / 256) * 256);
         pool_.p = probe_pool(pool_bytes, slot, stagger);
         TRITD_HIP(hipMemsetAsync(CE_.p, 0, CE_.bytes(), st_));
+        if (dy_) TRITD_HIP(hipMemsetAsync(CE2_.p, 0, CE2_.bytes(), st_));
         pool_.n = pool_bytes / sizeof(double);
         int q = 0;
         for (DBuf* b : {&D_, &O_, &E_, &YL_, &YO_, &T_}) {
@@ -288,6 +292,7 @@ IterScalars Session::scalars(int k) const {
     s.thr = o_.lambda / s.muO;
     s.den = s.muL + s.muO;
     s.invL_next = 1.0 / mu_[(size_t)k];
+    s.muO_prev = k >= 2 ? mu_[(size_t)k - 2] : 0.0;  // E^(0) = E^(-1) = 0: any value
     return s;
 }
 
@@ -367,7 +372,10 @@ void Session::launch_k5_any(int k, bool prologue) {
         return;
     }
     K5Args a{};
-    a.D = D_.p; a.O = O_.p; a.E = E_.p; a.CE = CE_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    a.D = D_.p; a.O = O_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
+    // E^(k-1) is read, E^(k) written (dy: over E^(k-2); otherwise in place)
+    a.E = e_buf(k - 1); a.CE = ce_buf(k - 1);
+    a.Ep = e_buf(k); a.CEp = ce_buf(k);
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
     a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
     a.ntt = g_.ntt;
@@ -375,7 +383,7 @@ void Session::launch_k5_any(int k, bool prologue) {
     a.stop = ctrl_;
     a.dense_tiles = dense_tiles();
     a.rot = rot_;
-    launch_k5(g_, a, prologue, st_);
+    launch_k5(g_, a, prologue, dy_, st_);
 }
 
 void Session::allreduce(double* buf, int64_t count) {
@@ -468,7 +476,7 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
                                         CE_.f(), st_);
                 else
                     launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[4],
-                                      (double*)f[5], CE_.p, st_);
+                                      (double*)f[5], CE_.p, dy_, st_);
             };
             probe();  // warm
             float ms = 1e30f;
@@ -712,17 +720,17 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
         if (f32_)
             launch_ce_expand32(g_, CE_.f(), E_.f(), st_);
         else
-            launch_ce_expand(g_, CE_.p, E_.p, st_);
+            launch_ce_expand(g_, ce_buf(done), e_buf(done), st_);
     }
     if ((O || E) && g_.n1l > 0) {
         DBuf tmp;
         tmp.alloc_bytes((size_t)(g_.n1l * g_.n2 * g_.n3) * es_);
-        for (auto pr : {std::make_pair(O, &O_), std::make_pair(E, &E_)}) {
+        for (auto pr : {std::make_pair(O, O_.p), std::make_pair(E, e_buf(done))}) {
             if (!pr.first) continue;
             if (f32_)
-                launch_from_tm32(g_, pr.second->f(), tmp.f(), g_.n1l, st_);
+                launch_from_tm32(g_, reinterpret_cast<float*>(pr.second), tmp.f(), g_.n1l, st_);
             else
-                launch_from_tm(g_, pr.second->p, tmp.p, g_.n1l, st_);
+                launch_from_tm(g_, pr.second, tmp.p, g_.n1l, st_);
             TRITD_HIP(hipMemcpy2DAsync(pr.first, ldOE * es_, tmp.p, g_.n1l * es_, g_.n1l * es_,
                                        (size_t)(g_.n2 * g_.n3), hipMemcpyDeviceToHost, st_));
             TRITD_HIP(hipStreamSynchronize(st_));

@@ -62,6 +62,10 @@ class Session {
     void rre_parts(const void* dX, int64_t ldX, double* num, double* den);
     bool is_f32() const { return f32_; }
     void counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch);
+    void k5_profile(int* dense_streams, int* slot_accesses) const {
+        *dense_streams = dy_ ? 4 : 6;
+        *slot_accesses = dy_ ? 3 : 2;
+    }
     void set_timing(bool on);
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
     const std::vector<double>& probe_ms() const { return probe_ms_; }
@@ -135,6 +139,13 @@ class Session {
     DBuf pool_;  // declared first: destroyed after the views into it
     DBuf D_, O_, E_, YL_, YO_, T_, Wk_;
     DBuf CE_;  // compact E slots (common.h)
+    // derived Y_O (k_admm.hip, fp64 default, TRITD_DY=0 disables): E^(k) lives
+    // in compact buffer k % 2 (CE_, CE2_) and dense buffer k % 2 (E_, and the
+    // pool slot of Y_O, which is not stored in this mode)
+    bool dy_ = false;
+    DBuf CE2_;
+    double* ce_buf(int k) const { return (dy_ && (k & 1)) ? CE2_.p : CE_.p; }
+    double* e_buf(int k) const { return (dy_ && (k & 1)) ? YO_.p : E_.p; }
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;

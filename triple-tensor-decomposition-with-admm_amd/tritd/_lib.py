@@ -66,6 +66,7 @@ SIGNATURES = {
     "tritd_session_kernel_ms": (C.c_int, [vp, dp, dp, dp, C.POINTER(i32)]),
     "tritd_session_probe": (C.c_int, [vp, dp, i32, C.POINTER(i32), C.POINTER(i32)]),
     "tritd_session_counters": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64)]),
+    "tritd_session_k5_profile": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32)]),
     "tritd_session_destroy": (None, [vp]),
     "tritd_comm_unique_id": (C.c_int, [vp]),
     "tritd_comm_create": (C.c_int, [C.POINTER(vp), vp, i32, i32, i32]),

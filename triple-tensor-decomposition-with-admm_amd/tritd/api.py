@@ -398,6 +398,12 @@ class Session:
         check(lib.tritd_session_counters(self._s, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def k5_profile(self):
+        """(dense N-streams per fused-update launch, compact-E slot accesses per tile)"""
+        a, b = _lib.i32(0), _lib.i32(0)
+        check(lib.tritd_session_k5_profile(self._s, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def set_timing(self, on=True):
         check(lib.tritd_session_set_timing(self._s, int(bool(on))))
 
