@@ -15,6 +15,11 @@ Per iteration k on the shard rows [i0, i1):
      L, O, E, Y_L, Y_O (:38-53), T_next (:33), W_next = T_next x3 C^
      red3 = [sum resL^2, sum resO^2]                           -> all-reduce
   D  errHist / stop test (:59-65)
+Y_O is not carried: like the fp64 fused update (k_admm.hip, derived Y_O) it
+is rebuilt each iteration as Y_L^(k-1) - mu_(k-1) (E^(k-1) - E^(k-2)).
+
+`sharded_als` is the same for triple_decomp_ALS.m (fit sum, [M2 | A^TA] and
+M3 reduced; als.cpp).
 """
 from __future__ import annotations
 
@@ -52,8 +57,8 @@ def sharded_admm(D_local, i0, i1, r, opts, A0, B0, C0, allreduce):
 
     O = np.zeros_like(D)
     E = np.zeros_like(D)
+    E_prev = np.zeros_like(D)
     YL = np.zeros_like(D)
-    YO = np.zeros_like(D)
     normD = float(np.sqrt(allreduce(np.array([np.sum(D * D)]))[0]))
     T = (D - O) + (1.0 / mus[0]) * YL
     W = np.einsum("ijt,tk->ijk", T, Ch)
@@ -73,16 +78,18 @@ def sharded_admm(D_local, i0, i1, r, opts, A0, B0, C0, allreduce):
         CtC = Ch.T @ Ch
 
         muL = muO = mus[k - 1]
+        mu_prev = mus[k - 2] if k >= 2 else 0.0
+        YO = YL - mu_prev * (E - E_prev)  # derived Y_O^(k-1) (k_admm.hip)
         L = np.einsum("ik,jk,tk->ijt", Ah, Bh, Ch)
         R1 = (D - L) + (1.0 / muL) * YL
         R2 = E - (1.0 / muO) * YO
         O = (muL * R1 + muO * R2) / (muL + muO)
         R3 = O + (1.0 / muO) * YO
+        E_prev = E
         E = np.sign(R3) * np.fmax(np.abs(R3) - lam / muO, 0.0)
         resL = (D - L) - O
         resO = O - E
         YL = YL + muL * resL
-        YO = YO + muO * resO
         T = (D - O) + (1.0 / mus[k]) * YL
         W = np.einsum("ijt,tk->ijk", T, Ch)
         ss = allreduce(np.array([np.sum(resL * resL), np.sum(resO * resO)]))
@@ -96,3 +103,38 @@ def sharded_admm(D_local, i0, i1, r, opts, A0, B0, C0, allreduce):
     B = np.transpose(Bh.reshape((n2, r, r), order="F"), (1, 0, 2)).copy(order="F")
     C = Ch.T.reshape((r, r, n3), order="F").copy(order="F")
     return dict(A_rows=A_loc, B=B, C=C, O=O, E=E, errHist=np.array(errHist), k=k)
+
+
+def sharded_als(X_local, i0, i1, r, opts, A0, B0, C0, allreduce):
+    """triple_decomp_ALS.m:1-40 on the shard rows [i0, i1) (als.cpp):
+    fit sum -> all-reduce -> errHist / stop; A local; [M2 | A^TA] and M3
+    all-reduced.  Returns the local A rows, replicated B, C, errHist, k."""
+    X = np.asarray(X_local, dtype=np.float64)
+    nl, n2, n3 = X.shape
+    R = r * r
+    Ah_full, Bh, Ch = _hat(A0, B0, C0, r)
+    Ah = Ah_full[i0:i1].copy()
+    maxIter, tol = int(opts["maxIter"]), float(opts["tol"])
+    Xnorm = float(np.sqrt(allreduce(np.array([np.sum(X * X)]))[0]))
+    ridge = 1e-9 * np.eye(R)
+    errHist = []
+    k = 0
+    for k in range(1, maxIter + 1):
+        L = np.einsum("ik,jk,tk->ijt", Ah, Bh, Ch)
+        ss = allreduce(np.array([np.sum((X - L) ** 2)]))
+        errHist.append(np.sqrt(ss[0]) / Xnorm)
+        if k > 1 and abs(errHist[-1] - errHist[-2]) < tol * errHist[-2]:
+            break
+        W = np.einsum("ijt,tk->ijk", X, Ch)
+        M1 = np.einsum("ijk,jk->ik", W, Bh)
+        Ah = M1 @ np.linalg.inv((Bh.T @ Bh) * (Ch.T @ Ch) + ridge)
+        red1 = allreduce(np.concatenate([np.einsum("ijk,ik->jk", W, Ah).ravel(),
+                                         (Ah.T @ Ah).ravel()]))
+        M2, AtA = red1[: n2 * R].reshape(n2, R), red1[n2 * R:].reshape(R, R)
+        Bh = M2 @ np.linalg.inv(AtA * (Ch.T @ Ch) + ridge)
+        M3 = allreduce(np.einsum("ijt,ik,jk->tk", X, Ah, Bh))
+        Ch = M3 @ np.linalg.inv(AtA * (Bh.T @ Bh) + ridge)
+    A_loc = Ah.reshape((nl, r, r), order="F")
+    B = np.transpose(Bh.reshape((n2, r, r), order="F"), (1, 0, 2)).copy(order="F")
+    C = Ch.T.reshape((r, r, n3), order="F").copy(order="F")
+    return dict(A_rows=A_loc, B=B, C=C, errHist=np.array(errHist), k=k)

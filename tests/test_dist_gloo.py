@@ -37,7 +37,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, outdir):
+def _worker(rank, world, port, name, outdir, kind="admm"):
     import sys
     for p in (PKG, ORACLE):
         sys.path.insert(0, p)
@@ -53,7 +53,7 @@ def _worker(rank, world, port, name, outdir):
     import json
     opts = json.loads(str(z["opts"]))
     r = int(z["r"])
-    D = z["D"]
+    D = z["D"] if kind == "admm" else z["X"]
     i0, i1 = shard_bounds(D.shape[0], world, rank)
 
     def allreduce(x):
@@ -61,8 +61,8 @@ def _worker(rank, world, port, name, outdir):
         dist.all_reduce(t)
         return t.numpy()
 
-    res = tritd_sharded.sharded_admm(D[i0:i1], i0, i1, r, opts, z["A0"], z["B0"], z["C0"],
-                                     allreduce)
+    run = tritd_sharded.sharded_admm if kind == "admm" else tritd_sharded.sharded_als
+    res = run(D[i0:i1], i0, i1, r, opts, z["A0"], z["B0"], z["C0"], allreduce)
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), i0=i0, i1=i1, **{
         k: v for k, v in res.items() if k != "k"}, k=res["k"])
     dist.barrier()
@@ -91,3 +91,22 @@ def test_sharded_schedule_world2_matches_golden(tmp_path, name):
     assert rel(A, g["A"]) < 1e-8
     assert rel(O, g["O"]) < 1e-9
     assert rel(E, g["E"]) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["als30_r3", "als20x24x18_r5_stop"])
+def test_sharded_als_world2_matches_golden(tmp_path, name):
+    """triple_decomp_ALS over 2 gloo ranks (the als.cpp schedule) == unsharded goldens."""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), name, str(tmp_path), "als"),
+                       nprocs=world, join=True, start_method="spawn")
+    g = load_golden(name)
+    A = np.zeros_like(g["A"])
+    for rank in range(world):
+        z = np.load(tmp_path / f"rank{rank}.npz")
+        i0, i1 = int(z["i0"]), int(z["i1"])
+        A[i0:i1] = z["A_rows"]
+        assert int(z["k"]) == g["k"]
+        assert rel(z["B"], g["B"]) < 1e-8 and rel(z["C"], g["C"]) < 1e-8
+        np.testing.assert_allclose(z["errHist"], g["errHist"], rtol=1e-9, atol=1e-14)
+    assert rel(A, g["A"]) < 1e-8
