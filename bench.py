@@ -3,7 +3,7 @@
 config 4, the default) or the 2048x2048x256 r=16 fp32 workload
 (configs[4] = config 5, ``--config 5``).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|5] [--algo admm|als]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A "step" is one ADMM iteration (triple_decomp_ADMM.m:31-66) over the whole
@@ -89,7 +89,11 @@ def main():
     # bounded host sample: ~20 s at config 4, one iteration at config 5 (§8d)
     ap.add_argument("--cpu-iters", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    # --algo als: triple_decomp_ALS.m on the config-4 workload
+    ap.add_argument("--algo", default="admm", choices=("admm", "als"))
     args = ap.parse_args()
+    if args.algo == "als":
+        return bench_als(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -254,6 +258,90 @@ def main():
         comm.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cpu_baseline_als(X, r, A0, B0, C0, iters):
+    """The numpy restatement of triple_decomp_ALS.m (oracle/tritd_oracle.py) on
+    a bounded sample of iterations (BLAS threads of numpy)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import tritd_oracle as orc
+        t0 = time.perf_counter()
+        *_, k = orc.triple_decomp_ALS(X, r, dict(maxIter=iters, tol=0.0), A0, B0, C0,
+                                      printer=lambda s: None)
+        dt = time.perf_counter() - t0
+        return {"value": k / dt, "unit": "iters/s",
+                "cores": int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1),
+                "kind": "port",
+                "sample": "%d ALS iterations of the same %dx%dx%d r=%d fp64 workload (numpy "
+                          "restatement of triple_decomp_ALS.m: buildF/G/H design matrices, "
+                          "unfold permutes, GEMM, SVD pinv)" % (k, *X.shape, r),
+                "seconds": dt}
+    except Exception as e:  # the baseline is reported, never the product
+        return {"value": None, "unit": "iters/s", "cores": 0, "kind": "port",
+                "sample": "unavailable: %s" % e}
+
+
+def bench_als(args):
+    """ALS iterations/s (triple_decomp_ALS.m:14-39) on the config-4 tensor,
+    one GPU, X resident in HBM.  Roofline on the fused fit kernel (L + error +
+    W = X x3 C^; 4 N R flops on f64 MFMA, N*8 B read)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--algo als runs on one GPU")
+    import torch
+    ensure_built()
+    import tritd
+    from tritd import synth
+    n1, n2, n3, r, _ = CONFIGS[4]
+    if args.n is not None:
+        n1 = n2 = n3 = args.n
+    r = args.r if args.r is not None else r
+    K, W = args.steps, args.warmup
+    data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    X = data["D"]
+    dev = torch.device("cuda", 0)
+    Xd = torch.from_numpy(np.ascontiguousarray(X.transpose(2, 1, 0))).to(dev)
+    opts = dict(maxIter=K + W, tol=0.0)  # tol 0: the stop test never fires in the timed region
+    s = tritd.AlsSession(r, opts, data["A0"], data["B0"], data["C0"], n1=n1, n2=n2, n3=n3,
+                         x_device_ptr=Xd.data_ptr(), ldX=n1, quiet=True)
+    del Xd
+    s.run(W)
+    s.sync()
+    s.set_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.run(K)
+    done, stopped = s.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    km = s.kernel_ms()
+    res = s.get()
+    N = n1 * n2 * n3
+    fit_flops = 4.0 * N * r * r
+    fit_bytes = N * 8 + r * r * n1 * n2 * 8
+    tfs = fit_flops / (km["fit"] * 1e-3) / 1e12 if km["fit"] > 0 else None
+    cpu = None if args.no_cpu else cpu_baseline_als(X, r, data["A0"], data["B0"], data["C0"],
+                                                    args.cpu_iters or 3)
+    line = {
+        "metric": "ALS iters/sec (triple_decomp_ALS.m), 512^3 r=8",
+        "value": K / dt, "unit": "iters/s", "n_gpus": 1, "steps": K, "warmup": W,
+        "ms_per_step": dt * 1e3 / K, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "triple_decomp_ALS on config 4: synthetic %dx%dx%d fp64 r=%d "
+                               "low-rank + 5%% outliers" % (n1, n2, n3, r),
+                   "n1": n1, "n2": n2, "n3": n3, "r": r, "parallelism": "mode1-shard x1"},
+        "errHist_final": float(res["errHist"][-1]), "k_final": res["k"],
+        "kernel_ms": {"fit": km["fit"], "mode3_mttkrp": km["mode3"],
+                      "iteration_events": km["iteration"], "samples": km["samples"]},
+        "roofline": {"bound": "mfma", "achieved": tfs, "peak": 78.6, "unit": "TFLOP/s",
+                     "frac": tfs / 78.6 if tfs else None, "traffic": None,
+                     "kernel": "k_als_fit (triple product + error + W)",
+                     "algorithmic_flops_per_launch": fit_flops,
+                     "hbm_achieved_GBs": fit_bytes / (km["fit"] * 1e-3) / 1e9 if km["fit"] else None},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    s.close()
 
 
 if __name__ == "__main__":
