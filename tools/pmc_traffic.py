@@ -6,7 +6,8 @@ the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE is
 exact for 16-B streaming stores.  Both counters are in KiB.
 
 usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [algorithmic_bytes [kernel]]
-(kernel: a substring of the kernel name, default k5_fused<64, false>)
+(kernel: a substring of the kernel name, default "k5_fused<64, false", which matches
+the stored-Y_O and the derived-Y_O instantiations)
 """
 import csv
 import glob
@@ -15,7 +16,7 @@ import os
 import sys
 
 
-def per_dispatch(d, counter, kname="k5_fused<64, false>"):
+def per_dispatch(d, counter, kname="k5_fused<64, false"):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
     for f in files:
@@ -32,7 +33,7 @@ def per_dispatch(d, counter, kname="k5_fused<64, false>"):
 def main():
     fd, wd, out = sys.argv[1:4]
     alg = float(sys.argv[4]) if len(sys.argv) > 4 else None
-    kname = sys.argv[5] if len(sys.argv) > 5 else "k5_fused<64, false>"
+    kname = sys.argv[5] if len(sys.argv) > 5 else "k5_fused<64, false"
     fetch = per_dispatch(fd, "FETCH_SIZE", kname)
     write = per_dispatch(wd, "WRITE_SIZE", kname)
     if not fetch or not write:

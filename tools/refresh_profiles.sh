@@ -7,7 +7,7 @@
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r01}
-ALG=${2:-6845104128}   # K5 algorithmic bytes per launch at 512^3 r=8 without dense E tiles
+ALG=${2:-4831874457}   # K5 algorithmic bytes per launch at 512^3 r=8, derived-Y_O mode (4 dense streams + compact-E slots + W)
 O=gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- \
@@ -20,3 +20,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sta
     python3 bench.py --no-cpu > $O/stats.log 2>&1
 timeout -k 10 400 python3 bench.py > $O/${TAG}_bench_line.json 2> $O/bench.err
 cat $O/${TAG}_bench_line.json
+# primitive kernels (unfold modes 2/3, soft_threshold, triple_product, evaluate, quality_ybz)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prims_stats -o run -- \
+    python3 tools/bench_prims.py > $O/${TAG}_prims.json 2> $O/prims.err
+cat $O/${TAG}_prims.json
