@@ -66,8 +66,13 @@ typedef struct {
     int32_t maxIter;  /* opts.maxIter */
     int32_t disp;     /* opts.disp    (print every 10 iterations, :60-62) */
     uint32_t present; /* TRITD_OPT_* bitmask */
-    uint32_t reserved;
+    uint32_t model;   /* opts.model (not read by the reference): TRITD_MODEL_CP (0, the executed
+                         rank-r^2 CP builders, fast_robust_triple_tensor/buildF.m) or TRITD_MODEL_QI
+                         (1, Qi's 3-index triple product of origin_triple_tensor/buildF.m:2-6,
+                         buildG.m:7-11, buildH.m:7-11; fp64, r <= 8; ADMM only) */
 } tritd_opts;
+
+enum { TRITD_MODEL_CP = 0, TRITD_MODEL_QI = 1 };
 
 /* Line printer used for opts.disp ("Iter %d, errL=%.2e, errO=%.2e").
  * Default: stdout.  MEX gateways install mexPrintf here. */
@@ -248,6 +253,15 @@ tritd_status tritd_als_sharded_virtual_f64(const double* X, int64_t n1, int64_t 
 /* ---------------------------------------------------------------------------
  * Primitives (host pointers).  Each replaces the named reference file.
  * ------------------------------------------------------------------------- */
+/* Qi-model triple product X(i,j,t) = sum_{p,q,s} A(i,q,s) B(p,j,s) C(p,q,t)
+ * (origin_triple_tensor/triple_product.m:8-19 as intended; equals
+ * reshape(unfold(A,1)*buildF(B,C)) with origin_triple_tensor/buildF.m:2-6).
+ * Host and device (stream) forms; r <= 16. */
+tritd_status tritd_triple_product_qi_f64(const double* A, const double* B, const double* C,
+                                         int64_t n1, int64_t n2, int64_t n3, int32_t r, double* X);
+tritd_status tritd_dev_triple_product_qi_f64(const double* A, const double* B, const double* C,
+                                             int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                                             double* X, void* stream);
 /* triple_product.m:1-7: X = reshape(unfold(A,1)*buildF(B,C), n1,n2,n3). */
 tritd_status tritd_triple_product_f64(const double* A, const double* B, const double* C, int64_t n1,
                                       int64_t n2, int64_t n3, int32_t r, double* X);

@@ -106,15 +106,73 @@ def buildH(A, B):
     return np.transpose(H, (1, 2, 0, 3)).reshape((r * r, n1 * n2), order="F")
 
 
-def triple_product(A, B, C):
-    """triple_product.m:1-7: Xhat = reshape(unfold(A,1)*buildF(B,C), n1,n2,n3)."""
+# ---------------------------------------------------------------------------
+# Qi-model design matrices (origin_triple_tensor/build{F,G,H}.m, SURVEY.md §8f
+# rank 4): the 3-index triple product L(i,j,t) = sum_{p,q,s} A(i,q,s)
+# B(p,j,s) C(p,q,t) that README line 43 describes ("single GEMM per mode").
+# In the reference these files are shadowed by the local CP builders of
+# origin_triple_tensor/triple_decomp_ADMM.m:166-194; here they back the opt-in
+# opts.model = 'qi' (restated exactly as the RPAS reshape-permute-GEMM).
+# ---------------------------------------------------------------------------
+def buildF_qi(B, C):
+    """origin_triple_tensor/buildF.m:2-6: F(q+(s-1)r, j+(t-1)n2) = sum_p B(p,j,s) C(p,q,t)."""
+    B = as3(B)
+    C = as3(C)
+    r, n2, _ = B.shape
+    n3 = C.shape[2]
+    F = np.transpose(B, (1, 2, 0)).reshape((n2 * r, r), order="F") @ C.reshape((r, r * n3), order="F")
+    F = np.transpose(F.reshape((n2, r, r, n3), order="F"), (2, 1, 0, 3))
+    return F.reshape((r * r, n2 * n3), order="F")
+
+
+def buildG_qi(A, C):
+    """origin_triple_tensor/buildG.m:7-11: G(p+(s-1)r, i+(t-1)n1) = sum_q A(i,q,s) C(p,q,t)."""
+    A = as3(A)
+    C = as3(C)
+    n1, r, _ = A.shape
+    n3 = C.shape[2]
+    G = (np.transpose(A, (0, 2, 1)).reshape((n1 * r, r), order="F")
+         @ np.transpose(C, (1, 0, 2)).reshape((r, r * n3), order="F"))
+    G = np.transpose(G.reshape((n1, r, r, n3), order="F"), (2, 1, 0, 3))
+    return G.reshape((r * r, n1 * n3), order="F")
+
+
+def buildH_qi(A, B):
+    """origin_triple_tensor/buildH.m:7-11: H(p+(q-1)r, i+(j-1)n1) = sum_s A(i,q,s) B(p,j,s)."""
+    A = as3(A)
+    B = as3(B)
+    n1, r, _ = A.shape
+    n2 = B.shape[1]
+    H = A.reshape((n1 * r, r), order="F") @ np.transpose(B, (2, 0, 1)).reshape((r, r * n2), order="F")
+    H = np.transpose(H.reshape((n1, r, r, n2), order="F"), (2, 1, 0, 3))
+    return H.reshape((r * r, n1 * n2), order="F")
+
+
+def kronF(B, C):
+    """origin_triple_tensor/kronF.m:1-7: the explicit-Kronecker form of the Qi F
+    (rows ordered s+(q-1)r instead of buildF's q+(s-1)r)."""
+    B = as3(B)
+    C = as3(C)
+    r, n2, _ = B.shape
+    B1 = np.kron(np.eye(r), unfold(np.transpose(B, (2, 1, 0)), 1))
+    C1 = np.kron(C.reshape((r * r, C.shape[2]), order="F"), np.eye(n2))
+    return B1 @ C1
+
+
+BUILDERS = {"cp": None, "qi": None}  # filled below (model -> (buildF, buildG, buildH))
+
+
+def triple_product(A, B, C, model="cp"):
+    """triple_product.m:1-7: Xhat = reshape(unfold(A,1)*buildF(B,C), n1,n2,n3).
+    model='qi': the same statement with origin_triple_tensor/buildF.m, i.e. the
+    3-index sum origin_triple_tensor/triple_product.m:8-19 intends."""
     A = as3(A)
     B = as3(B)
     C = as3(C)
     n1 = A.shape[0]
     n2 = B.shape[1]
     n3 = C.shape[2]
-    X = unfold(A, 1) @ buildF(B, C)
+    X = unfold(A, 1) @ BUILDERS[model][0](B, C)
     return X.reshape((n1, n2, n3), order="F")
 
 
@@ -177,27 +235,27 @@ def reshape_C_from_C3(C3, n3, r):
     return C
 
 
-def update_A(X, A, B, C, alphaA):
+def update_A(X, A, B, C, alphaA, model="cp"):
     """triple_decomp_ADMM.m:73-81."""
     X1 = unfold(X, 1)
-    F = buildF(B, C)
+    F = BUILDERS[model][0](B, C)
     G = F @ F.T + alphaA * np.eye(F.shape[0])
     A1 = (X1 @ F.T) @ pinv(G)
     return reshape_A_from_A1(A1, A.shape[0], A.shape[1])
 
 
-def update_B(X, A, B, C, alphaB):
+def update_B(X, A, B, C, alphaB, model="cp"):
     """triple_decomp_ADMM.m:83-88."""
     X2 = unfold(X, 2)
-    G = buildG(A, C)
+    G = BUILDERS[model][1](A, C)
     B_old_unf = (X2 @ G.T) @ pinv(G @ G.T + alphaB * np.eye(G.shape[0]))
     return reshape_B_from_B2(B_old_unf, B.shape[1], B.shape[0])
 
 
-def update_C(X, A, B, C):
+def update_C(X, A, B, C, model="cp"):
     """triple_decomp_ADMM.m:90-95 (ridge hard-coded to 1e-9 at :93)."""
     X3 = unfold(X, 3)
-    H = buildH(A, B)
+    H = BUILDERS[model][2](A, B)
     C_old_unf = (X3 @ H.T) @ pinv(H @ H.T + 1e-9 * np.eye(H.shape[0]))
     return reshape_C_from_C3(C_old_unf, C.shape[2], C.shape[0])
 
@@ -211,6 +269,17 @@ def check_opts(opts):
     for f in REQUIRED_OPTS:
         if f not in opts:
             raise KeyError(f"Reference to non-existent field '{f}'.")
+
+
+def opts_model(opts):
+    """Opt-in model switch (not read by the reference): absent or 'cp' = the
+    executed code (rank-r^2 CP, fast_robust_triple_tensor/buildF.m); 'qi' =
+    the Qi-model builders of origin_triple_tensor/ (SURVEY.md §8f rank 4)."""
+    m = opts.get("model", "cp") if hasattr(opts, "get") else "cp"
+    m = str(m).lower()
+    if m not in BUILDERS:
+        raise ValueError("opts.model must be 'cp' or 'qi'")
+    return m
 
 
 def triple_decomp_ADMM(D, r, opts, A0, B0, C0, trace_iters=(), printer=None):
@@ -229,6 +298,7 @@ def triple_decomp_ADMM(D, r, opts, A0, B0, C0, trace_iters=(), printer=None):
     lam = float(opts["lambda"])                                      # :18
     lambda2 = float(opts["lambda2"])                                 # :19
     maxIter = int(opts["maxIter"]); tol = float(opts["tol"]); disp = bool(opts["disp"])  # :20
+    model = opts_model(opts)
 
     A = as3(A0).reshape((n1, r, r), order="F").copy(order="F")      # :23
     B = as3(B0).reshape((r, n2, r), order="F").copy(order="F")
@@ -244,11 +314,11 @@ def triple_decomp_ADMM(D, r, opts, A0, B0, C0, trace_iters=(), printer=None):
     k = 0
     for k in range(1, maxIter + 1):                                  # :31
         T = (D - O) + (1.0 / muL) * Y_L                               # :33
-        A = update_A(T, A, B, C, lambda2)                             # :34
-        B = update_B(T, A, B, C, lambda2)                             # :35
-        C = update_C(T, A, B, C)                                      # :36
+        A = update_A(T, A, B, C, lambda2, model)                      # :34
+        B = update_B(T, A, B, C, lambda2, model)                      # :35
+        C = update_C(T, A, B, C, model)                               # :36
 
-        L = triple_product(A, B, C)                                   # :38
+        L = triple_product(A, B, C, model)                            # :38
 
         R1 = (D - L) + (1.0 / muL) * Y_L                              # :41
         R2 = E - (1.0 / muO) * Y_O                                    # :42
@@ -478,4 +548,54 @@ def triple_product_loops(A, B, C):
                     for q in range(A.shape[2]):
                         s = s + A[i, p, q] * B[p, j, q] * C[p, q, t]
                 X[i, j, t] = s
+    return X
+
+
+BUILDERS["cp"] = (buildF, buildG, buildH)
+BUILDERS["qi"] = (buildF_qi, buildG_qi, buildH_qi)
+
+
+def buildG_qi_loops(A, C):
+    """origin_triple_tensor/buildG.m:2-6 (comment): G(p+(s-1)r, i+(t-1)n1) = sum_q A(i,q,s) C(p,q,t)."""
+    n1, r, _ = A.shape
+    n3 = C.shape[2]
+    G = np.zeros((r * r, n1 * n3), order="F")
+    for i in range(n1):
+        for t in range(n3):
+            for p in range(r):
+                for s_ in range(r):
+                    G[p + s_ * r, i + t * n1] = sum(A[i, q, s_] * C[p, q, t] for q in range(r))
+    return G
+
+
+def buildH_qi_loops(A, B):
+    """origin_triple_tensor/buildH.m:2-6 (comment): H(p+(q-1)r, i+(j-1)n1) = sum_s A(i,q,s) B(p,j,s)."""
+    n1, r, _ = A.shape
+    n2 = B.shape[1]
+    H = np.zeros((r * r, n1 * n2), order="F")
+    for i in range(n1):
+        for j in range(n2):
+            for p in range(r):
+                for q in range(r):
+                    H[p + q * r, i + j * n1] = sum(A[i, q, s_] * B[p, j, s_] for s_ in range(r))
+    return H
+
+
+def triple_product_qi_loops(A, B, C):
+    """origin_triple_tensor/triple_product.m:8-19: total += a(i,q,s)*b(p,j,s)*c(p,q,t)
+    (the file indexes undefined lower-case a/b/c — a MATLAB error as written;
+    this is the sum it spells out, with A, B, C)."""
+    n1, r, _ = A.shape
+    n2 = B.shape[1]
+    n3 = C.shape[2]
+    X = np.zeros((n1, n2, n3), order="F")
+    for i in range(n1):
+        for j in range(n2):
+            for t in range(n3):
+                tot = 0.0
+                for p in range(r):
+                    for q in range(r):
+                        for s_ in range(r):
+                            tot = tot + A[i, q, s_] * B[p, j, s_] * C[p, q, t]
+                X[i, j, t] = tot
     return X

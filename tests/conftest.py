@@ -21,8 +21,9 @@ def pytest_configure(config):
 
 
 def golden_names(kind="admm"):
-    """Committed golden cases: triple_decomp_ADMM (g*.npz) or triple_decomp_ALS (als*.npz)."""
-    pat = {"admm": "g*.npz", "als": "als*.npz"}[kind]
+    """Committed golden cases: triple_decomp_ADMM (g*.npz), the same solver with
+    opts.model='qi' (qi*.npz) or triple_decomp_ALS (als*.npz)."""
+    pat = {"admm": "g*.npz", "qi": "qi*.npz", "als": "als*.npz"}[kind]
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, pat)))
 
 

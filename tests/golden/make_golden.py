@@ -43,6 +43,16 @@ CASES = {
     # r=8 exercises the R=64 (full MFMA tile) code path at a small size
     "g17x16x20_r8": (synth.low_rank_plus_outliers, dict(n1=17, n2=16, n3=20, r=8), 8,
                      dict(synth.TRAFFIC_OPTS, maxIter=25), False),
+    # opts.model = 'qi' (SURVEY.md §8f rank 4): Qi-model builders of
+    # origin_triple_tensor/, data drawn from the Qi triple product
+    "qi12x10x8_r2": (synth.low_rank_plus_outliers, dict(n1=12, n2=10, n3=8, r=2, model="qi"), 2,
+                     dict(synth.TRAFFIC_OPTS, maxIter=30, model="qi"), True),
+    "qi30_r3": (synth.low_rank_plus_outliers, dict(n1=30, n2=30, n3=30, r=3, model="qi"), 3,
+                dict(synth.TRAFFIC_OPTS, model="qi"), False),
+    "qi17x16x20_r8": (synth.low_rank_plus_outliers, dict(n1=17, n2=16, n3=20, r=8, model="qi"), 8,
+                      dict(synth.TRAFFIC_OPTS, maxIter=25, model="qi"), False),
+    "qi20x24x18_r3_video_stop": (synth.video_like, dict(n1=20, n2=24, n3=18, r=3), 3,
+                                 dict(synth.VIDEO_OPTS, maxIter=60, tol=0.1, model="qi"), False),
 }
 
 
@@ -92,10 +102,12 @@ def make(name):
 
 
 if __name__ == "__main__":
-    # python tests/golden/make_golden.py [admm|als]  (default: both)
+    # python tests/golden/make_golden.py [admm|qi|als]  (default: all)
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
-    if which in ("all", "admm"):
+    if which in ("all", "admm", "qi"):
         for n in CASES:
+            if which == "qi" and not n.startswith("qi"):
+                continue
             print(n, *make(n))
     if which in ("all", "als"):
         for n in ALS_CASES:

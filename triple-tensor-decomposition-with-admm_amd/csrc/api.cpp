@@ -741,6 +741,49 @@ tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, cons
     });
 }
 
+// Qi model: H (k_qi.hip) is the Khatri-Rao operand of the same kernel
+tritd_status tritd_dev_triple_product_qi_f64(const double* A, const double* B, const double* C,
+                                             int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                                             double* X, void* stream) {
+    return guarded([&] {
+        check_dims(n1, n2, n3, r, true);
+        need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
+        hipStream_t st = as_stream(stream);
+        Geom g = make_geom(n1, n2, n3, 0, n1, r);
+        g.RP = padded_rank32(g.R);
+        DBuf Ah, Bh, ChT, H, ones;
+        Ah.alloc((size_t)(g.n1p * g.RP));
+        Bh.alloc((size_t)(n2 * g.RP));
+        ChT.alloc((size_t)g.RP * g.n3p);
+        H.alloc((size_t)(g.n1p * n2 * g.RP));
+        ones.alloc((size_t)g.RP);
+        launch_pack_factors(g, A, B, C, Ah.p, Bh.p, ChT.p, st);
+        launch_fill(ones.p, g.RP, 1.0, st);
+        launch_qi_h(g, r, Ah.p, Bh.p, H.p, nullptr, st);
+        launch_tp(g, H.p, ones.p, ChT.p, X, nullptr, nullptr, 0, n1, n1 * n2, st, g.n1p * g.RP, 0);
+        TRITD_HIP(hipStreamSynchronize(st));
+    });
+}
+
+tritd_status tritd_triple_product_qi_f64(const double* A, const double* B, const double* C,
+                                         int64_t n1, int64_t n2, int64_t n3, int32_t r, double* X) {
+    return guarded([&] {
+        check_dims(n1, n2, n3, r, true);
+        need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
+        pick_device(-1);
+        const int64_t R = (int64_t)r * r;
+        DBuf dA, dB, dC, dX;
+        dA.alloc(n1 * R); dB.alloc(R * n2); dC.alloc(R * n3); dX.alloc((size_t)(n1 * n2 * n3));
+        TRITD_HIP(hipMemcpy(dA.p, A, dA.n * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dB.p, B, dB.n * 8, hipMemcpyHostToDevice));
+        TRITD_HIP(hipMemcpy(dC.p, C, dC.n * 8, hipMemcpyHostToDevice));
+        const tritd_status s =
+            tritd_dev_triple_product_qi_f64(dA.p, dB.p, dC.p, n1, n2, n3, r, dX.p, nullptr);
+        if (s != TRITD_OK) throw Error(s, g_last_error);
+        TRITD_HIP(hipMemcpy(X, dX.p, dX.n * 8, hipMemcpyDeviceToHost));
+    });
+}
+
 tritd_status tritd_triple_product_f64(const double* A, const double* B, const double* C, int64_t n1,
                                       int64_t n2, int64_t n3, int32_t r, double* X) {
     return guarded([&] {

@@ -247,7 +247,7 @@ void k5_fused(K5Args a) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int k = 4 * s + tg;
-            kr[s] = active ? a.Ah[i * RP + k] * a.Bh[j * RP + k] : 0.0;
+            kr[s] = active ? a.Ah[j * a.ahj + i * RP + k] * a.Bh[j * a.bhj + k] : 0.0;  // CP or Qi (kernels.h)
         }
     }
     d4 wacc[MT];

@@ -113,7 +113,8 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
                                                const double* __restrict__ Ah,
                                                const double* __restrict__ Bh, double* part,
                                                int64_t n1p, int64_t n3p, int64_t ntt,
-                                               int64_t tiles, int S, const int* stop) {
+                                               int64_t tiles, int S, const int* stop,
+                                               int64_t ahj, int64_t bhj) {
     if (*stop) return;
     constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -154,13 +155,14 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
         if (g + 1 < g1) loadB(g + 1);
         const int64_t j = g / qper;
         const int64_t i0 = (g - j * qper) << 4;
+        const double* Aj = Ah + j * ahj;  // Qi model: rows of H (kernels.h)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
             const int k = 16 * m + il;
-            const double bh = Bh[j * RP + k];
+            const double bh = Bh[j * bhj + k];
             double a[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) a[s] = Ah[(i0 + 4 * s + tg) * RP + k] * bh;
+            for (int s = 0; s < 4; ++s) a[s] = Aj[(i0 + 4 * s + tg) * RP + k] * bh;
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -243,7 +245,8 @@ int m3_split(const Geom& g) {
 int m3_parts(const Geom& g) { return m3_split(g) / 4; }
 
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
-               double* M3, const int* stop, hipStream_t st) {
+               double* M3, const int* stop, hipStream_t st, int64_t ahj, int64_t bhj) {
+    if (bhj < 0) bhj = g.RP;
     const int S = m3_split(g);
     const int64_t ntb = cdiv(g.ntt, 4);
     const dim3 grid((unsigned)(ntb * S / 4));
@@ -257,7 +260,7 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
             attr_set = true;                                                                  \
         }                                                                                     \
         hipLaunchKernelGGL(k_m3<RPV>, grid, dim3(256), lds, st, T, Ah, Bh, part, g.n1p, g.n3p, \
-                           g.ntt, g.tiles, S, stop);                                          \
+                           g.ntt, g.tiles, S, stop, ahj, bhj);                                \
     } break;
     switch (g.RP) {
         M3_CASE(16)

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
                                                       const double* __restrict__ X, double* partial,
                                                       int64_t n1p, int64_t n1l, int64_t n3,
                                                       int64_t n3p, int64_t tiles, int64_t ldj,
-                                                      int64_t ldt) {
+                                                      int64_t ldt, int64_t ahj, int64_t bhj) {
     constexpr int KS = RP / 4;
     constexpr int LDT = TPC + 16;  // 2*LDT = 96 = 32 mod 64 dwords: no bank conflicts per half-wave
     __shared__ double cs[RP * LDT];
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
         const int k = 4 * s + tg;
-        kr[s] = active ? Ah[i * RP + k] * Bh[j * RP + k] : 0.0;
+        kr[s] = active ? Ah[j * ahj + i * RP + k] * Bh[j * bhj + k] : 0.0;  // kernels.h: KR source
     }
     const int64_t obase = i + ldj * j;
     double sn = 0.0, sd = 0.0;
@@ -143,16 +143,17 @@ int tp_grid(const Geom& g) { return (int)cdiv(g.tiles, TP_WAVES); }
 
 void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
                const double* X, double* partial, int mode, int64_t ldj, int64_t ldt,
-               hipStream_t st) {
+               hipStream_t st, int64_t ahj, int64_t bhj) {
+    if (bhj < 0) bhj = g.RP;
     const dim3 grid(tp_grid(g)), block(64 * TP_WAVES);
 #define TP_CASE(RPV)                                                                            \
     case RPV:                                                                                   \
         if (mode == 0)                                                                          \
             hipLaunchKernelGGL((k_tp<RPV, 0>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
-                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt);                  \
+                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt, ahj, bhj);                  \
         else                                                                                    \
             hipLaunchKernelGGL((k_tp<RPV, 1>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
-                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt);                  \
+                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt, ahj, bhj);                  \
         break;
     switch (g.RP) {
         TP_CASE(16)

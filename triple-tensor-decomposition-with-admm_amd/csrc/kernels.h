@@ -39,6 +39,10 @@ struct K5Args {
     // E^(k-1) (CEp/Ep) and writes E^(k+1) over E^(k-1) (k_admm.hip)
     double* CEp;
     double* Ep;
+    // Khatri-Rao operand source: kr(ij,k) = Ah[j*ahj + i*RP + k] * Bh[j*bhj + k].
+    // CP (the executed model): ahj = 0, bhj = RP.  Qi model (opts.model='qi'):
+    // Ah = H (k_qi.hip, rows j*n1p+i), ahj = n1p*RP, Bh = ones, bhj = 0.
+    int64_t ahj, bhj;
 };
 int k5_grid(const Geom& g);
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st);
@@ -67,8 +71,9 @@ void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, c
                hipStream_t st);
 int m3_split(const Geom& g);
 int m3_parts(const Geom& g);  // partial slabs of n3p*RP written by K2
+// kr(ij,k) = Ah[j*ahj + i*RP + k] * Bh[j*bhj + k] (K5Args::ahj; bhj < 0 means RP)
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
-               double* M3, const int* stop, hipStream_t st);
+               double* M3, const int* stop, hipStream_t st, int64_t ahj = 0, int64_t bhj = -1);
 // G = X^T X over `rows` rows of a row-major [rows][RP] factor
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop, hipStream_t st);
 // Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere)
@@ -77,6 +82,21 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
 // Y = M * Ginv ([rows][RP]); optional transposed copy YT[k*ldT + i]
 void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, double* Y, double* YT,
                   int64_t ldT, const int* stop, hipStream_t st);
+// ---- Qi model (opts.model='qi', k_qi.hip; origin_triple_tensor/build{F,G,H}.m) ----
+// H[(j*n1p+i)*RP + p+r*q] = sum_s Ah(i, q+r*s) Bh(j, p+r*s)  (zero for k >= R)
+void launch_qi_h(const Geom& g, int r, const double* Ah, const double* Bh, double* H,
+                 const int* stop, hipStream_t st);
+// M1(i, q+r*s) = sum_j sum_p W(ij, p+r*q) Bh(j, p+r*s)
+void launch_m1_qi(const Geom& g, int r, const double* Wk, const double* Bh, double* M1,
+                  const int* stop, hipStream_t st);
+// M2(j, p+r*s) = sum_i sum_q W(ij, p+r*q) Ah(i, q+r*s)
+void launch_m2_qi(const Geom& g, int r, const double* Wk, const double* AhT, double* M2,
+                  const int* stop, hipStream_t st);
+// F F' / G G' / H H' of the Qi design matrices from the factor Grams
+// (mode 0: X=B^TB, Y=C^TC; 1: X=A^TA, Y=C^TC; 2: X=A^TA, Y=B^TB)
+void launch_qi_gram(int RP, int r, int mode, const double* X, const double* Y, double* out,
+                    const int* stop, hipStream_t st);
+void launch_fill(double* x, int64_t n, double v, hipStream_t st);
 // out = sum_p in[p] (fixed order), written back to every in[p]  (virtual shards)
 void launch_vsum(double* const* bufs, int nbufs, int64_t count, hipStream_t st);
 
@@ -91,7 +111,7 @@ int sumsq_blocks(const Geom& g);
 int tp_grid(const Geom& g);
 void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
                const double* X, double* partial, int mode, int64_t ldj, int64_t ldt,
-               hipStream_t st);
+               hipStream_t st, int64_t ahj = 0, int64_t bhj = -1);
 // reference-layout device factors A (n1,r,r), B (r,n2,r), C (r,r,n3) -> Ah, Bh, ChT
 void launch_pack_factors(const Geom& g, const double* A, const double* B, const double* C,
                          double* Ah, double* Bh, double* ChT, hipStream_t st);

@@ -100,6 +100,11 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         for (hipEvent_t* e : {&evAtA_, &evBtB_, &evCtC_, &evSA_, &evSB_, &evSC_})
             TRITD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
+    qi_ = o_.model == TRITD_MODEL_QI;
+    if (o_.model != TRITD_MODEL_CP && o_.model != TRITD_MODEL_QI)
+        throw Error(TRITD_ERR_ARG, "opts.model must be 'cp' or 'qi'");
+    if (qi_ && f32_)
+        throw Error(TRITD_ERR_UNSUPPORTED, "opts.model='qi' is implemented for a double D only");
     if (f32_ ? !rp_supported32(g_.RP) : !rp_supported(g_.RP))
         throw Error(TRITD_ERR_UNSUPPORTED,
                     f32_ ? "r must be in 1..16 for the fp32 path" : "r must be in 1..8 for the fp64 path");
@@ -157,6 +162,13 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     }
     BtB_.alloc((size_t)g_.RP * g_.RP);
     CtC_.alloc((size_t)g_.RP * g_.RP);
+    if (qi_) {
+        H_.alloc((size_t)(g_.n1p * g_.n2 * g_.RP));
+        TRITD_HIP(hipMemsetAsync(H_.p, 0, H_.bytes(), st_));
+        ones_.alloc((size_t)g_.RP * g_.RP);
+        launch_fill(ones_.p, (int64_t)ones_.n, 1.0, st_);
+        for (DBuf* b : {&GqA_, &GqB_, &GqC_}) b->alloc((size_t)g_.RP * g_.RP);
+    }
     red1_.alloc(red1_count());
     red2_.alloc(red2_count());
     red3_.alloc(2);
@@ -215,7 +227,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     if (overlap_ || shov_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
         TRITD_HIP(hipEventRecord(evCtC_, st_));
         TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-        launch_solve(g_.RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+        solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
         TRITD_HIP(hipEventRecord(evSA_, side_));
         TRITD_HIP(hipStreamSynchronize(side_));
     }
@@ -311,24 +323,47 @@ IterScalars32 Session::scalars32(int k) const {
 }
 
 void Session::do_m1() {
-    if (f32_)
+    if (qi_)
+        launch_m1_qi(g_, g_.r, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    else if (f32_)
         launch_m1_32(g_, Wk_.f(), Bh_.p, M1_.f(), ctrl_, st_);
     else
         launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
 }
 
 void Session::do_m2(double* M2) {
-    if (f32_)
+    if (qi_)
+        launch_m2_qi(g_, g_.r, Wk_.p, AhT_.p, M2, ctrl_, st_);
+    else if (f32_)
         launch_m2_32(g_, Wk_.f(), AhT_.p, M2, ctrl_, st_);
     else
         launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
 }
 
 void Session::do_m3() {
-    if (f32_)
+    if (qi_)
+        do_m3_qi();
+    else if (f32_)
         launch_m3_32(g_, T_.f(), Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
     else
         launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
+}
+
+// Qi: H from the fresh A^, B^ (after update_B); read by K2 and by the K5 that follows
+void Session::do_m3_qi() {
+    launch_qi_h(g_, g_.r, Ah_.p, Bh_.p, H_.p, ctrl_, st_);
+    launch_m3(g_, T_.p, H_.p, ones_.p, m3part_.p, red2_.p, ctrl_, st_, g_.n1p * g_.RP, 0);
+}
+
+void Session::solve(int mode, const double* P, const double* Q, double alpha, double* out,
+                    hipStream_t s) {
+    if (!qi_) {
+        launch_solve(g_.RP, g_.R, P, Q, alpha, out, ctrl_ + 2, ctrl_, s);
+        return;
+    }
+    double* G = (mode == 0 ? GqA_ : mode == 1 ? GqB_ : GqC_).p;
+    launch_qi_gram(g_.RP, g_.r, mode, P, Q, G, ctrl_, s);
+    launch_solve(g_.RP, g_.R, G, ones_.p, alpha, out, ctrl_ + 2, ctrl_, s);
 }
 
 // (X*F')*pinv(G): fp64 path through the MFMA apply (RP <= 64); fp32
@@ -377,6 +412,11 @@ void Session::launch_k5_any(int k, bool prologue) {
     a.E = e_buf(k - 1); a.CE = ce_buf(k - 1);
     a.Ep = e_buf(k); a.CEp = ce_buf(k);
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
+    a.ahj = 0; a.bhj = g_.RP;
+    if (qi_) {  // L = H Ch^T (H built before K2 of this iteration)
+        a.Ah = H_.p; a.Bh = ones_.p;
+        a.ahj = g_.n1p * g_.RP; a.bhj = 0;
+    }
     a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
     a.ntt = g_.ntt;
     a.s = scalars(k);
@@ -404,7 +444,7 @@ void Session::phaseA(int k) {
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
     do_m1();
-    launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, Ginv_.p, ctrl_ + 2, ctrl_, st_);
+    solve(0, BtB_.p, CtC_.p, o_.lambda2, Ginv_.p, st_);
     do_apply_A(Ginv_.p);
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     do_m2(M2);
@@ -415,7 +455,7 @@ void Session::phaseB(int k) {
     const int RP = g_.RP;
     const double* M2 = red1_.p;
     const double* AtA = red1_.p + g_.n2 * RP;
-    launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, Ginv_.p, ctrl_ + 2, ctrl_, st_);
+    solve(1, AtA, CtC_.p, o_.lambda2, Ginv_.p, st_);
     do_apply_B(M2, Ginv_.p);
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
@@ -426,7 +466,7 @@ void Session::phaseB(int k) {
 void Session::phaseC(int k) {
     const int RP = g_.RP;
     const double* AtA = red1_.p + g_.n2 * RP;
-    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :93 ridge
+    solve(2, AtA, BtB_.p, 1e-9, Ginv_.p, st_);  // :93 ridge
     do_apply_C(Ginv_.p);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     launch_k5_full(k, /*fused_finish=*/false);
@@ -532,7 +572,7 @@ void Session::iterate_overlapped(int k) {
     TRITD_HIP(hipEventRecord(evAtA_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
     if (gs == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
-    launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, GinvB_.p, ctrl_ + 2, ctrl_, side_);
+    solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, side_);
     TRITD_HIP(hipEventRecord(evSB_, side_));
     do_m2(M2);
     TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
@@ -541,7 +581,7 @@ void Session::iterate_overlapped(int k) {
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
     if (gs == side_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
-    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, side_);  // :93 ridge
+    solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
     do_m3();
@@ -552,7 +592,7 @@ void Session::iterate_overlapped(int k) {
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
     if (gs == side_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
-    launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+    solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/true);
 }
@@ -575,12 +615,12 @@ void Session::iterate_sharded(int k) {
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     do_m2(M2);
     allreduce(red1_.p, red1_count());
-    launch_solve(RP, g_.R, AtA, CtC_.p, o_.lambda2, GinvB_.p, ctrl_ + 2, ctrl_, st_);
+    solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
     do_apply_B(M2, GinvB_.p);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
-    launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, side_);  // :93 ridge
+    solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
     do_m3();
@@ -591,7 +631,7 @@ void Session::iterate_sharded(int k) {
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
-    launch_solve(RP, g_.R, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, ctrl_ + 2, ctrl_, side_);
+    solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/false);
     allreduce(red3_.p, 2);
@@ -766,7 +806,13 @@ void Session::rre_parts(const void* dX, int64_t ldX, double* num, double* den) {
     part.alloc(2 * (size_t)grid);
     out.alloc(2);
     // X(i,j,t) of the shard at src[i + ldX*(j + n2*t)]
-    launch_tp(g_, Ah_.p, Bh_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_);
+    if (qi_) {
+        launch_qi_h(g_, g_.r, Ah_.p, Bh_.p, H_.p, nullptr, st_);
+        launch_tp(g_, H_.p, ones_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_,
+                  g_.n1p * g_.RP, 0);
+    } else {
+        launch_tp(g_, Ah_.p, Bh_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_);
+    }
     launch_reduce_pairs(part.p, grid, out.p, nullptr, st_);
     double h[2];
     TRITD_HIP(hipMemcpyAsync(h, out.p, sizeof h, hipMemcpyDeviceToHost, st_));

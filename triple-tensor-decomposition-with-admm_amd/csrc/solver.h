@@ -118,6 +118,7 @@ class Session {
     void do_m1();
     void do_m2(double* M2);
     void do_m3();
+    void do_m3_qi();
     void do_apply_A(const double* Ginv);
     void do_apply_B(const double* M2, const double* Ginv);
     void do_apply_C(const double* Ginv);
@@ -147,6 +148,15 @@ class Session {
     double* ce_buf(int k) const { return (dy_ && (k & 1)) ? CE2_.p : CE_.p; }
     double* e_buf(int k) const { return (dy_ && (k & 1)) ? YO_.p : E_.p; }
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
+    // Qi model (opts.model = TRITD_MODEL_QI, k_qi.hip): H = the Qi mode-3 design
+    // matrix by rows ij (K2/K5 Khatri-Rao operand), an all-ones RP x RP block
+    // (the Hadamard factor of the solve and the B operand of the KR product),
+    // and the design Grams of the three solves
+    bool qi_ = false;
+    DBuf H_, ones_, GqA_, GqB_, GqC_;
+    // inv(design Gram + alpha I) of update_A (mode 0), _B (1), _C (2)
+    void solve(int mode, const double* P, const double* Q, double alpha, double* out,
+               hipStream_t s);
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;
     DBuf errHist_, errL_, errO_;

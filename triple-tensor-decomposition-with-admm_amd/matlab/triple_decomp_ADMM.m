@@ -11,6 +11,11 @@ function [A, B, C, O, errHist, E] = triple_decomp_ADMM(D, r, opts)
 %   O and E single, A, B, C and errHist double, as MATLAB's class rules give
 %   the reference); any other class is processed in double.  Use
 %   tritd_devices(idx) to shard D over several GPUs.
+%
+%   opts.model = 'qi' (optional; this build's own field) swaps the executed
+%   rank-r^2 CP builders for the Qi-model design matrices of
+%   origin_triple_tensor/buildF.m, buildG.m, buildH.m (3-index triple
+%   product; reconstruct with triple_product(A, B, C, 'qi')).  Double D only.
 [n1, n2, n3] = size(D);
 A0 = randn(n1, r, r);
 B0 = randn(r, n2, r);

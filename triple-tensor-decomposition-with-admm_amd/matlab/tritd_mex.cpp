@@ -8,7 +8,7 @@
 //                         triple_decomp_ALS (double X) -> tritd_als_f64
 //   tritd_mex('devices', idx)  HIP device ordinals (0-based) the next solves
 //                         shard D over (tritd_set_devices; [] clears)
-//   X  = tritd_mex('triple_product', A, B, C)
+//   X  = tritd_mex('triple_product', A, B, C[, 'qi'])
 //   Xn = tritd_mex('unfold', X, mode)
 //   Y  = tritd_mex('soft_threshold', X, lam)
 //
@@ -64,6 +64,22 @@ bool read_opts(const mxArray* s, tritd_opts* o, std::string* err) {
             case TRITD_OPT_DISP: o->disp = x != 0.0; break;
         }
         o->present |= f.bit;
+    }
+    // opts.model (this build's own field): 'cp' (default) or 'qi'
+    o->model = TRITD_MODEL_CP;
+    if (const mxArray* m = mxGetField(s, 0, "model")) {
+        char buf[8] = {0};
+        if (!mxIsChar(m) || mxGetString(m, buf, sizeof buf) != 0) {
+            *err = "opts.model must be 'cp' or 'qi'";
+            return false;
+        }
+        const std::string v(buf);
+        if (v == "qi" || v == "QI")
+            o->model = TRITD_MODEL_QI;
+        else if (v != "cp" && v != "CP") {
+            *err = "opts.model must be 'cp' or 'qi'";
+            return false;
+        }
     }
     return true;
 }
@@ -232,16 +248,26 @@ void do_devices(int, mxArray*[], int nrhs, const mxArray* prhs[]) {
 }
 
 void do_triple_product(int, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
-    if (nrhs != 4) fail("tritd:nargin", "usage: tritd_mex('triple_product', A, B, C)");
+    if (nrhs != 4 && nrhs != 5)
+        fail("tritd:nargin", "usage: tritd_mex('triple_product', A, B, C[, 'qi'])");
+    bool qi = false;
+    if (nrhs == 5) {
+        char buf[8] = {0};
+        if (!mxIsChar(prhs[4]) || mxGetString(prhs[4], buf, sizeof buf) != 0 ||
+            (std::string(buf) != "qi" && std::string(buf) != "cp"))
+            fail("tritd:model", "model must be 'cp' or 'qi'");
+        qi = std::string(buf) == "qi";
+    }
     for (int k = 1; k < 4; ++k) need_double(prhs[k], "factor");
     int64_t a[3], b[3], c[3];
     std::string err;
     if (!size3(prhs[1], a, &err) || !size3(prhs[2], b, &err) || !size3(prhs[3], c, &err))
         fail("tritd:dims", err);
     mxArray* X = make3(a[0], b[1], c[2]);
-    const tritd_status st = tritd_triple_product_f64(mxGetPr(prhs[1]), mxGetPr(prhs[2]),
-                                                     mxGetPr(prhs[3]), a[0], b[1], c[2],
-                                                     (int32_t)a[1], mxGetPr(X));
+    const tritd_status st =
+        (qi ? tritd_triple_product_qi_f64 : tritd_triple_product_f64)(
+            mxGetPr(prhs[1]), mxGetPr(prhs[2]), mxGetPr(prhs[3]), a[0], b[1], c[2], (int32_t)a[1],
+            mxGetPr(X));
     if (st != TRITD_OK) {
         mxDestroyArray(X);
         fail("tritd:triple_product", status_msg(st));

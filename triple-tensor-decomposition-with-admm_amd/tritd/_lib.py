@@ -21,6 +21,7 @@ STATUS_NAMES = {0: "TRITD_OK", 1: "TRITD_ERR_ARG", 2: "TRITD_ERR_OPTS", 3: "TRIT
 OPT_MU, OPT_RHO, OPT_LAMBDA, OPT_LAMBDA2, OPT_MAXITER, OPT_TOL, OPT_DISP = (1 << i for i in range(7))
 OPT_BITS = {"mu": OPT_MU, "rho": OPT_RHO, "lambda": OPT_LAMBDA, "lambda2": OPT_LAMBDA2,
             "maxIter": OPT_MAXITER, "tol": OPT_TOL, "disp": OPT_DISP}
+MODELS = {"cp": 0, "qi": 1}  # opts.model: TRITD_MODEL_CP / TRITD_MODEL_QI (include/tritd.h)
 SESSION_D_ON_DEVICE = 1
 SESSION_F32 = 2
 
@@ -34,7 +35,7 @@ class TritdError(RuntimeError):
 class Opts(C.Structure):
     _fields_ = [("mu", C.c_double), ("rho", C.c_double), ("lambda_", C.c_double),
                 ("lambda2", C.c_double), ("tol", C.c_double), ("maxIter", C.c_int32),
-                ("disp", C.c_int32), ("present", C.c_uint32), ("reserved", C.c_uint32)]
+                ("disp", C.c_int32), ("present", C.c_uint32), ("model", C.c_uint32)]
 
 
 PRINT_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
@@ -99,6 +100,8 @@ SIGNATURES = {
     "tritd_dev_unfold_f64": (C.c_int, [vp, i64, i64, i64, i32, vp, vp]),
     "tritd_dev_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp, vp]),
     "tritd_dev_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp, vp]),
+    "tritd_triple_product_qi_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp]),
+    "tritd_dev_triple_product_qi_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp, vp]),
 }
 
 

@@ -6,7 +6,7 @@ the MATLAB file it replaces and runs on the GPU through libtritd.so:
     triple_decomp_ADMM(D, r, opts)          fast_robust_triple_tensor/triple_decomp_ADMM.m:1
     triple_decomp_ADMM_outlier(D, r, opts)  alias expected at video_triple_comparison.m:54
     triple_decomp_ALS(X, r, opts)           fast_robust_triple_tensor/triple_decomp_ALS.m:1
-    triple_product(A, B, C)                 triple_product.m:1
+    triple_product(A, B, C[, model])        triple_product.m:1 (model='qi': origin_triple_tensor/)
     unfold(X, mode)                         unfold.m:1
     soft_threshold(X, lam)                  soft_threshold.m:1
     buildF(B, C) / buildG(A, C) / buildH(A, B)   buildF.m:1 / buildG.m:1 / buildH.m:1
@@ -17,7 +17,10 @@ Arrays are numpy, MATLAB (column-major) semantics.  `opts` is a dict (or any
 object with attributes) holding the fields the reference reads
 (mu, rho, lambda, lambda2, maxIter, tol, disp); a missing one raises
 ``KeyError("Reference to non-existent field 'x'.")`` like MATLAB, extras
-(alphaA, alphaB, origin, ...) are ignored.
+(alphaA, alphaB, origin, ...) are ignored.  One optional field is this
+build's own: ``opts.model`` = 'cp' (default: the executed rank-r^2 CP builders)
+or 'qi' (Qi's 3-index triple product, origin_triple_tensor/build{F,G,H}.m;
+SURVEY.md §8f rank 4).
 """
 from __future__ import annotations
 
@@ -54,7 +57,18 @@ def make_opts(opts):
     o.maxIter = int(_get(opts, "maxIter"))
     o.disp = int(bool(_get(opts, "disp")))
     o.present = present
+    o.model = model_code(_get(opts, "model"))
     return o
+
+
+def model_code(m):
+    """opts.model -> TRITD_MODEL_*: absent/'cp' -> 0, 'qi' -> 1."""
+    if m is None:
+        return 0
+    key = str(m).lower()
+    if key not in _lib.MODELS:
+        raise ValueError("opts.model must be 'cp' or 'qi'")
+    return _lib.MODELS[key]
 
 
 def _f64(X):
@@ -221,8 +235,10 @@ def triple_decomp_ALS(X, r, opts, A0=None, B0=None, C0=None, *, device=-1, retur
     return tuple(out)
 
 
-def triple_product(A, B, C_):
-    """Xhat = triple_product(A, B, C)  (triple_product.m:1-7)."""
+def triple_product(A, B, C_, model="cp"):
+    """Xhat = triple_product(A, B, C)  (triple_product.m:1-7).  model='qi': Qi's
+    3-index product sum_{p,q,s} A(i,q,s)B(p,j,s)C(p,q,t)
+    (origin_triple_tensor/triple_product.m:8-19, buildF.m:2-6)."""
     A = _fortran(A)
     B = _fortran(B)
     C_ = _fortran(C_)
@@ -230,7 +246,8 @@ def triple_product(A, B, C_):
     n2 = _size3(B)[1]
     n3 = _size3(C_)[2]
     X = np.zeros((n1, n2, n3), order="F")
-    check(lib.tritd_triple_product_f64(_ptr(A), _ptr(B), _ptr(C_), n1, n2, n3, r, _ptr(X)))
+    fn = lib.tritd_triple_product_qi_f64 if model_code(model) else lib.tritd_triple_product_f64
+    check(fn(_ptr(A), _ptr(B), _ptr(C_), n1, n2, n3, r, _ptr(X)))
     return X
 
 

@@ -46,6 +46,12 @@ def cp_full(Ah, Bh, Ch):
     return (Ah @ KR.T).reshape((n1, n2, n3), order="F")
 
 
+def qi_full(A, B, C):
+    """Qi-model triple product L(i,j,t) = sum_{p,q,s} A(i,q,s) B(p,j,s) C(p,q,t)
+    (origin_triple_tensor/triple_product.m:8-19; opts.model='qi')."""
+    return np.asfortranarray(np.einsum("iqs,pjs,pqt->ijt", A, B, C, optimize=True))
+
+
 def random_factors(n1, n2, n3, r, seed):
     rng = np.random.default_rng(seed)
     A = np.asfortranarray(rng.standard_normal((n1, r, r)))
@@ -54,13 +60,14 @@ def random_factors(n1, n2, n3, r, seed):
     return A, B, C
 
 
-def low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123):
-    """Config 1/4/5 generator.  Returns dict(D, Lstar, A0, B0, C0)."""
+def low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123, model="cp"):
+    """Config 1/4/5 generator.  Returns dict(D, Lstar, A0, B0, C0).
+    model='qi' draws L* from the Qi-model triple product instead."""
     rng = np.random.default_rng(seed)
     As = np.asfortranarray(rng.standard_normal((n1, r, r)))
     Bs = np.asfortranarray(rng.standard_normal((r, n2, r)))
     Cs = np.asfortranarray(rng.standard_normal((r, r, n3)))
-    Lstar = cp_full(*hat_factors(As, Bs, Cs))
+    Lstar = qi_full(As, Bs, Cs) if model == "qi" else cp_full(*hat_factors(As, Bs, Cs))
     sigma = float(Lstar.std())
     support = rng.random((n1, n2, n3)) < p_out
     vals = rng.uniform(-10.0 * sigma, 10.0 * sigma, size=(n1, n2, n3))
