@@ -228,6 +228,22 @@ tritd_status tritd_als_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, 
  * [i0, i1) as for tritd_session_create; flags: TRITD_SESSION_D_ON_DEVICE).
  * quiet = 1 skips the every-5-iterations progress line (and its host
  * synchronisation). */
+/* Nonconvex variant, fast_robust_triple_tensor/test.m:1-73 (the file's function
+ * is named triple_decomp_ADMM_outlier(X, r, rho, lambda, gamma_A, epsilon, p, theta,
+ * maxIter, tol)).  Outlier ADMM over Y = X - O with duals
+ * Lambda, Gamma, while A, B, C follow an ALS on X (ridge 1e-12 + reweighted
+ * shrink on A, 1e-9 on B, C).  errHist(k) = ||X - Y - O||/||X|| after the updates,
+ * printed every iteration ("Iteration %d, relative error = %.4e"); on the stop
+ * test errHist holds *iters entries and O is that of iteration *iters - 1
+ * (the reference breaks before O = O_new).  X, O column-major n1 x n2 x n3;
+ * factors as tritd_admm_f64; errHist capacity maxIter; fp64, r <= 8.
+ * device < 0: the device set (tritd_set_devices) or the current device. */
+tritd_status tritd_ncvx_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                           double rho, double lambda, double gamma_A, double epsilon, double p,
+                           double theta, int32_t maxIter, double tol, const double* A0,
+                           const double* B0, const double* C0, double* A, double* B, double* C,
+                           double* O, double* errHist, int32_t* iters, int32_t device);
+
 typedef struct tritd_als_session tritd_als_session;
 tritd_status tritd_als_session_create(tritd_als_session** out, int32_t device, const double* X,
                                       int64_t ldX, int64_t n1, int64_t n2, int64_t n3, int64_t i0,

@@ -352,6 +352,83 @@ def triple_decomp_ADMM(D, r, opts, A0, B0, C0, trace_iters=(), printer=None):
     return A, B, C, O, errHist, E, k, trace
 
 
+# ---------------------------------------------------------------------------
+# Nonconvex variant: fast_robust_triple_tensor/test.m.
+# The file defines `triple_decomp_ADMM_outlier(X, r, rho, lambda, gamma_A,
+# epsilon, p, theta, maxIter, tol)` with its own local helpers (`:77-211`):
+# a Y-split ADMM for the outliers O, while A, B, C follow an ALS on the data X
+# itself with a reweighted (l_p-like) soft threshold on A.
+# ---------------------------------------------------------------------------
+def weighted_soft_threshold(X, tau, W):
+    """test.m:97-101: sign(X).*max(abs(X) - tau.*W, 0)."""
+    return matlab_sign(X) * matlab_max0(np.abs(X) - tau * W)
+
+
+def ncvx_update_A(X, A, B, C, gamma_A, epsilon, p, theta):
+    """test.m:77-92: ridge 1e-12, then the reweighted shrink of A1."""
+    X1 = unfold(X, 1)
+    F = buildF(B, C)
+    A_old_unf = (X1 @ F.T) @ pinv(F @ F.T + 1e-12 * np.eye(F.shape[0]))      # :82
+    W_A = 1.0 / ((np.abs(A_old_unf) + epsilon) ** (theta - p))                 # :86
+    A_new_unf = weighted_soft_threshold(A_old_unf, gamma_A, W_A)               # :89
+    return reshape_A_from_A1(A_new_unf, A.shape[0], A.shape[1])                # :92
+
+
+def ncvx_update_B(X, A, B, C):
+    """test.m:114-119 (ridge 1e-9 at :117)."""
+    X2 = unfold(X, 2)
+    G = buildG(A, C)
+    B_old_unf = (X2 @ G.T) @ pinv(G @ G.T + 1e-9 * np.eye(G.shape[0]))
+    return reshape_B_from_B2(B_old_unf, B.shape[1], B.shape[0])
+
+
+def triple_decomp_ADMM_ncvx(X, r, rho, lam, gamma_A, epsilon, p, theta, maxIter, tol,
+                            A0, B0, C0, printer=None, trace_iters=()):
+    """Restatement of fast_robust_triple_tensor/test.m:1-73.
+
+    Returns ``(A, B, C, O, errHist, k, trace)``; the reference returns the
+    first five.  Semantics kept: T uses the factors from the start of the
+    iteration (`:35`); the factor updates read X, never Y or O (`:49-51`);
+    errHist(k) = ||X - Y_new - O_new||/||X|| (`:62`) is printed every
+    iteration (`:63`); on the stop test (`:65-68`) errHist is truncated and
+    the loop breaks BEFORE `O = O_new` (`:71`), so the returned O is that of
+    iteration k-1 while A, B, C are those of iteration k; without a break
+    errHist keeps all maxIter entries.  W_O is all ones (`:43`)."""
+    X = as3(X)
+    n1, n2, n3 = X.shape                                              # :19
+    Xnorm = np.linalg.norm(X.ravel(order="F"))                        # :20
+    A = as3(A0).reshape((n1, r, r), order="F").copy(order="F")       # :24-26
+    B = as3(B0).reshape((r, n2, r), order="F").copy(order="F")
+    C = as3(C0).reshape((r, r, n3), order="F").copy(order="F")
+    O = np.zeros((n1, n2, n3), order="F")                             # :28
+    Lam = np.zeros((n1, n2, n3), order="F")                           # :29
+    Gam = np.zeros((n1, n2, n3), order="F")                           # :30
+    errHist = np.zeros(int(maxIter))                                  # :32
+    trace = {}
+    k = 0
+    for k in range(1, int(maxIter) + 1):                              # :34
+        T = triple_product(A, B, C)                                   # :35
+        Y_new = ((X - O) + rho * (T + Lam / rho)) / (1 + rho)         # :36
+        W_O = np.ones(O.shape)                                        # :43
+        O_new = weighted_soft_threshold((X - Y_new) + Gam / rho, lam / rho, W_O)   # :44
+        Lam = Lam + rho * (T - Y_new)                                 # :47
+        Gam = Gam + rho * ((X - Y_new) - O_new)                       # :48
+        A = ncvx_update_A(X, A, B, C, gamma_A, epsilon, p, theta)     # :49
+        B = ncvx_update_B(X, A, B, C)                                 # :50
+        C = update_C(X, A, B, C)                                      # :51 (same ridge 1e-9, :124)
+        errHist[k - 1] = np.linalg.norm(((X - Y_new) - O_new).ravel(order="F")) / Xnorm   # :62
+        (printer or print)("Iteration %d, relative error = %.4e" % (k, errHist[k - 1]))  # :63
+        if k in trace_iters:
+            trace[k] = dict(A=A.copy(order="F"), B=B.copy(order="F"), C=C.copy(order="F"),
+                            O=O_new.copy(order="F"), Lam=Lam.copy(order="F"),
+                            Gam=Gam.copy(order="F"))
+        if k > 1 and abs(errHist[k - 1] - errHist[k - 2]) < tol * errHist[k - 2]:  # :65
+            errHist = errHist[:k]                                     # :66
+            break                                                     # :67 (O keeps iteration k-1)
+        O = O_new                                                     # :71
+    return A, B, C, O, errHist, k, trace
+
+
 def triple_decomp_ALS(X, r, opts, A0, B0, C0, printer=None):
     """Restatement of fast_robust_triple_tensor/triple_decomp_ALS.m:1-40.
 

@@ -22,8 +22,9 @@ def pytest_configure(config):
 
 def golden_names(kind="admm"):
     """Committed golden cases: triple_decomp_ADMM (g*.npz), the same solver with
-    opts.model='qi' (qi*.npz) or triple_decomp_ALS (als*.npz)."""
-    pat = {"admm": "g*.npz", "qi": "qi*.npz", "als": "als*.npz"}[kind]
+    opts.model='qi' (qi*.npz), triple_decomp_ALS (als*.npz) or the nonconvex
+    test.m solver (nc*.npz)."""
+    pat = {"admm": "g*.npz", "qi": "qi*.npz", "als": "als*.npz", "ncvx": "nc*.npz"}[kind]
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, pat)))
 
 

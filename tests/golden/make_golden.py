@@ -70,6 +70,40 @@ ALS_CASES = {
 }
 
 
+# fast_robust_triple_tensor/test.m (nonconvex variant):
+# positional parameters (rho, lambda, gamma_A, epsilon, p, theta, maxIter, tol);
+# the reference has no caller, so these values are this build's choice
+NCVX_PARAMS = dict(rho=1.0, **{"lambda": 0.5}, gamma_A=1e-3, epsilon=1e-2, p=0.5, theta=2.0 / 3.0)
+NCVX_CASES = {
+    "nc12x10x8_r2": (synth.low_rank_plus_outliers, dict(n1=12, n2=10, n3=8, r=2), 2,
+                     dict(NCVX_PARAMS, maxIter=30, tol=1e-5)),
+    "nc30_r3": (synth.low_rank_plus_outliers, dict(n1=30, n2=30, n3=30, r=3), 3,
+                dict(NCVX_PARAMS, maxIter=60, tol=1e-5)),
+    "nc17x16x20_r8": (synth.low_rank_plus_outliers, dict(n1=17, n2=16, n3=20, r=8), 8,
+                      dict(NCVX_PARAMS, maxIter=25, tol=1e-5)),
+    # the stop test fires: errHist truncated, O of the previous iteration returned
+    "nc20x24x18_r3_stop": (synth.video_like, dict(n1=20, n2=24, n3=18, r=3), 3,
+                           dict(NCVX_PARAMS, rho=0.5, maxIter=60, tol=2e-2)),
+}
+
+
+def make_ncvx(name):
+    gen, kw, r, prm = NCVX_CASES[name]
+    d = gen(**kw)
+    A, B, C, O, eh, k, tr = orc.triple_decomp_ADMM_ncvx(
+        d["D"], r, prm["rho"], prm["lambda"], prm["gamma_A"], prm["epsilon"], prm["p"],
+        prm["theta"], prm["maxIter"], prm["tol"], d["A0"], d["B0"], d["C0"],
+        printer=lambda s: None, trace_iters=(1, 2))
+    out = dict(X=d["D"], A0=d["A0"], B0=d["B0"], C0=d["C0"], r=np.int64(r),
+               opts=np.array(json.dumps(prm)), A=A, B=B, C=C, O=O, errHist=eh, k=np.int64(k))
+    if name == "nc12x10x8_r2":  # the state after iterations 1 and 2 (localises a divergence)
+        for it in (1, 2):
+            for key in ("A", "B", "C", "O"):
+                out[f"it{it}_{key}"] = tr[it][key]
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    return k, eh[-1]
+
+
 def make_als(name):
     gen, kw, r, opts = ALS_CASES[name]
     d = gen(**kw)
@@ -102,7 +136,7 @@ def make(name):
 
 
 if __name__ == "__main__":
-    # python tests/golden/make_golden.py [admm|qi|als]  (default: all)
+    # python tests/golden/make_golden.py [admm|qi|als|ncvx]  (default: all)
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "admm", "qi"):
         for n in CASES:
@@ -112,3 +146,6 @@ if __name__ == "__main__":
     if which in ("all", "als"):
         for n in ALS_CASES:
             print(n, *make_als(n))
+    if which in ("all", "ncvx"):
+        for n in NCVX_CASES:
+            print(n, *make_ncvx(n))

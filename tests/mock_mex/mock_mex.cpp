@@ -153,7 +153,11 @@ int mock_admm(const void* D, long n1, long n2, long n3, int r, const char* opt_n
         while (pos <= names.size() && !names.empty()) {
             const size_t c = names.find(',', pos);
             const std::string nm = names.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
-            opts->fields[nm] = dbl(&opt_vals[q++], {1, 1});
+            const size_t eq = nm.find('=');
+            if (eq != std::string::npos)  // "model=qi": a char field, no value consumed
+                opts->fields[nm.substr(0, eq)] = cmd_arg(nm.substr(eq + 1).c_str());
+            else
+                opts->fields[nm] = dbl(&opt_vals[q++], {1, 1});
             if (c == std::string::npos) break;
             pos = c + 1;
         }
@@ -229,6 +233,42 @@ int mock_als(const double* X, long n1, long n2, long n3, int r, const char* opt_
         std::memcpy(C, out[2]->data.data(), (size_t)r * r * n3 * 8);
         *k = (int)out[3]->dims[0];
         std::memcpy(errHist, out[3]->data.data(), (size_t)*k * 8);
+    } catch (const MockMexError& e) {
+        std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
+        rc = 1;
+    }
+    std::snprintf(printed, printlen, "%s", g_printed.c_str());
+    for (auto* a : in) mxDestroyArray(a);
+    for (auto* a : out)
+        if (a) mxDestroyArray(a);
+    return rc;
+}
+
+// tritd_mex('ncvx', X, r, rho, lambda, gamma_A, epsilon, p, theta, maxIter, tol, A0, B0, C0)
+int mock_ncvx(const double* X, long n1, long n2, long n3, int r, const double* prm8,
+              const double* A0, const double* B0, const double* C0, double* A, double* B,
+              double* C, double* O, double* errHist, int* k, char* err, int errlen, char* printed,
+              int printlen) {
+    std::vector<mxArray*> in;
+    in.push_back(cmd_arg("ncvx"));
+    in.push_back(dbl(X, {(mwSize)n1, (mwSize)n2, (mwSize)n3}));
+    double rr = r;
+    in.push_back(dbl(&rr, {1, 1}));
+    for (int q = 0; q < 8; ++q) in.push_back(dbl(&prm8[q], {1, 1}));
+    in.push_back(dbl(A0, {(mwSize)n1, (mwSize)r, (mwSize)r}));
+    in.push_back(dbl(B0, {(mwSize)r, (mwSize)n2, (mwSize)r}));
+    in.push_back(dbl(C0, {(mwSize)r, (mwSize)r, (mwSize)n3}));
+    mxArray* out[5] = {nullptr};
+    int rc = 0;
+    g_printed.clear();
+    try {
+        mexFunction(5, out, (int)in.size(), const_cast<const mxArray**>(in.data()));
+        std::memcpy(A, out[0]->data.data(), (size_t)n1 * r * r * 8);
+        std::memcpy(B, out[1]->data.data(), (size_t)r * n2 * r * 8);
+        std::memcpy(C, out[2]->data.data(), (size_t)r * r * n3 * 8);
+        std::memcpy(O, out[3]->data.data(), (size_t)n1 * n2 * n3 * 8);
+        *k = (int)out[4]->dims[0];
+        std::memcpy(errHist, out[4]->data.data(), (size_t)*k * 8);
     } catch (const MockMexError& e) {
         std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
         rc = 1;

@@ -179,3 +179,65 @@ def test_gateway_als_matches_golden(gw, name):
     lines = res["printed"].splitlines()
     assert lines == ["Iteration %d, relative error = %.4e" % (i, g["errHist"][i - 1])
                      for i in range(5, g["k"] + 1, 5)]
+
+
+# ---------------------------------------------------------------------------
+# opts.model = 'qi' and the nonconvex 'ncvx' command
+# ---------------------------------------------------------------------------
+def test_gateway_bad_model_is_refused(gw):
+    g = load_golden("qi12x10x8_r2")
+    names = ["mu", "rho", "lambda", "lambda2", "maxIter", "tol", "disp"]
+    rc, err, _ = run(gw, g, names + ["model=tucker"], [float(g["opts"][n]) for n in names])
+    assert rc == 1 and err == "tritd:opts|opts.model must be 'cp' or 'qi'"
+
+
+@pytest.mark.gpu
+def test_gateway_qi_matches_golden(gw):
+    import tritd_oracle as orc
+    g = load_golden("qi30_r3")
+    names = ["mu", "rho", "lambda", "lambda2", "maxIter", "tol", "disp"]
+    rc, err, res = run(gw, g, names + ["model=qi"], [float(g["opts"][n]) for n in names])
+    assert rc == 0, err
+    assert res["k"] == g["k"]
+    L = orc.triple_product(res["A"], res["B"], res["C"], "qi")
+    assert rel(L, orc.triple_product(g["A"], g["B"], g["C"], "qi")) <= 1e-9
+    assert rel(res["O"], g["O"]) <= 1e-9
+
+
+def run_ncvx(gw, g):
+    X = np.asfortranarray(g["X"])
+    n1, n2, n3 = X.shape
+    r = g["r"]
+    o = g["opts"]
+    prm = np.array([o[n] for n in ("rho", "lambda", "gamma_A", "epsilon", "p", "theta",
+                                   "maxIter", "tol")], dtype=np.float64)
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cc = np.zeros((r, r, n3), order="F")
+    O = np.zeros_like(X)
+    eh = np.zeros(int(o["maxIter"]) + 1)
+    k = C.c_int(0)
+    err = C.create_string_buffer(1024)
+    pr = C.create_string_buffer(1 << 16)
+    p = lambda a: C.c_void_p(a.ctypes.data)
+    A0, B0, C0 = (np.asfortranarray(g[x]) for x in ("A0", "B0", "C0"))
+    rc = gw.mock_ncvx(p(X), n1, n2, n3, r, p(prm), p(A0), p(B0), p(C0), p(A), p(B), p(Cc), p(O),
+                      p(eh), C.byref(k), err, 1024, pr, 1 << 16)
+    return rc, err.value.decode(), dict(A=A, B=B, C=Cc, O=O, errHist=eh[: k.value], k=k.value,
+                                        printed=pr.value.decode())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["nc30_r3", "nc20x24x18_r3_stop"])
+def test_gateway_ncvx_matches_golden(gw, name):
+    import tritd_oracle as orc
+    g = load_golden(name)
+    rc, err, res = run_ncvx(gw, g)
+    assert rc == 0, err
+    assert res["k"] == g["k"]
+    assert rel(orc.triple_product(res["A"], res["B"], res["C"]),
+               orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
+    assert rel(res["O"], g["O"]) <= 1e-9
+    np.testing.assert_allclose(res["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
+    lines = [ln for ln in res["printed"].splitlines() if ln.startswith("Iteration ")]
+    assert len(lines) == g["k"]  # test.m:63 prints every iteration

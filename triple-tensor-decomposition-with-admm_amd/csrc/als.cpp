@@ -130,14 +130,34 @@ int AlsSession::next_iter() {
     return ++k_enq_;
 }
 
+void AlsSession::enable_ncvx(const NcvxParams& p) {
+    TRITD_HIP(hipSetDevice(device_));
+    ncvx_ = true;
+    np_ = p;
+    const size_t Np = (size_t)g_.Ntm;
+    for (DBuf* b : {&Oa_, &Ob_, &Lam_, &Gam_}) {
+        b->alloc(Np);
+        TRITD_HIP(hipMemsetAsync(b->p, 0, Np * sizeof(double), st_));
+    }
+}
+
 void AlsSession::phaseFit(int k) {
-    (void)k;
     AlsFitArgs a{};
     a.X = X_.p; a.Wk = Wk_.p; a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p;
     a.partial = fitpart_.p;
     a.n1p = g_.n1p; a.n2 = g_.n2; a.n3p = g_.n3p; a.plane = g_.plane; a.tiles = g_.tiles;
     a.ntt = g_.ntt;
     a.stop = ctrl_;
+    if (ncvx_) {  // test.m:35-48; O of iteration k-1 in buffer (k-1)&1, O of k into k&1
+        a.ncvx = 1;
+        a.O_in = ((k - 1) & 1) ? Ob_.p : Oa_.p;
+        a.O_out = (k & 1) ? Ob_.p : Oa_.p;
+        a.Lam = Lam_.p;
+        a.Gam = Gam_.p;
+        a.rho = np_.rho;
+        a.tau = np_.lambda / np_.rho;  // lambda/rho (:44); tau.*W_O = tau (W_O = ones, :43)
+        a.onep = 1.0 + np_.rho;        // (1 + rho) (:36)
+    }
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
     launch_als_fit(g_, a, st_);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
@@ -145,6 +165,14 @@ void AlsSession::phaseFit(int k) {
 }
 
 void AlsSession::phaseErr(int k) {
+    if (ncvx_) return;  // test.m takes errHist after the updates: phaseEnd
+    launch_als_finish(red0_.p, Xnorm_, k, tol_, errHist_.p, ctrl_, st_);
+}
+
+void AlsSession::phaseEnd(int k) {
+    if (!ncvx_) return;
+    // errHist(k) = norm(X(:) - Y_new(:) - O_new(:))/Xnorm (:62); the stop flag
+    // set here makes every kernel of k+1 exit (:65-67)
     launch_als_finish(red0_.p, Xnorm_, k, tol_, errHist_.p, ctrl_, st_);
 }
 
@@ -154,8 +182,12 @@ void AlsSession::phaseA(int k) {
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
     launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
-    launch_solve(RP, g_.R, BtB_.p, CtC_.p, 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);  // :27
+    // ALS :27 ridge 1e-9; test.m:82 ridge 1e-12, then the reweighted shrink :86-89
+    launch_solve(RP, g_.R, BtB_.p, CtC_.p, ncvx_ ? 1e-12 : 1e-9, Ginv_.p, ctrl_ + 2, ctrl_, st_);
     launch_apply(RP, M1_.p, g_.n1p, Ginv_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    if (ncvx_)
+        launch_ncvx_shrink(g_, Ah_.p, AhT_.p, np_.gamma_A, np_.epsilon, np_.theta - np_.p, ctrl_,
+                           st_);
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
 }
@@ -183,7 +215,7 @@ void AlsSession::phaseC(int k) {
 }
 
 void AlsSession::maybe_print(int k) {
-    if (quiet_ || k % 5 != 0) return;  // :17
+    if (quiet_ || (!ncvx_ && k % 5 != 0)) return;  // ALS :17; test.m:63 prints every iteration
     if (comm_ && comm_->rank != 0) return;
     int ctrl[2];
     double e;
@@ -192,7 +224,7 @@ void AlsSession::maybe_print(int k) {
     TRITD_HIP(hipStreamSynchronize(st_));
     if (ctrl[1] != k) return;  // the loop broke before iteration k
     char line[128];
-    std::snprintf(line, sizeof line, "Iteration %d, relative error = %.4e", k, e);  // :18
+    std::snprintf(line, sizeof line, "Iteration %d, relative error = %.4e", k, e);  // :18 (test.m:63)
     emit_line(line);
 }
 
@@ -211,12 +243,14 @@ void AlsSession::run(int iters) {
         phaseFit(k);
         allreduce(red0_.p, 2);
         phaseErr(k);
-        maybe_print(k);
+        if (!ncvx_) maybe_print(k);
         phaseA(k);
         allreduce(red1_.p, red1_count());
         phaseB(k);
         allreduce(red2_.p, red2_count());
         phaseC(k);
+        phaseEnd(k);
+        if (ncvx_) maybe_print(k);
         if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 1], st_));
     }
 }
@@ -283,6 +317,24 @@ void AlsSession::get(double* A, double* B, double* C, double* errHist, int* iter
         TRITD_HIP(hipMemcpy(errHist, errHist_.p, (size_t)done * sizeof(double),
                             hipMemcpyDeviceToHost));
     if (iters) *iters = done;
+}
+
+void AlsSession::get_O(double* O, int64_t ldO) {
+    int done = 0, stopped = 0;
+    sync(&done, &stopped);
+    if (!ncvx_) throw Error(TRITD_ERR_STATE, "get_O: not a nonconvex (test.m) session");
+    // :67 breaks before O = O_new (:71): a stop at k returns O of k-1
+    const int kk = stopped ? done - 1 : done;
+    const double* src = (kk & 1) ? Ob_.p : Oa_.p;  // kk = 0: the zero initial O
+    if (g_.n1l > 0) {
+        DBuf tmp;
+        tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));
+        launch_from_tm(g_, src, tmp.p, g_.n1l, st_);
+        TRITD_HIP(hipMemcpy2DAsync(O, ldO * sizeof(double), tmp.p, g_.n1l * sizeof(double),
+                                   g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
+                                   hipMemcpyDeviceToHost, st_));
+        TRITD_HIP(hipStreamSynchronize(st_));
+    }
 }
 
 }  // namespace tritd

@@ -7,6 +7,12 @@
 
 namespace tritd {
 
+// Parameters of the nonconvex solver of fast_robust_triple_tensor/test.m:1
+// (positional in the reference: rho, lambda, gamma_A, epsilon, p, theta).
+struct NcvxParams {
+    double rho, lambda, gamma_A, epsilon, p, theta;
+};
+
 class AlsSession {
    public:
     // X: double, column-major shard rows [i0, i1) with leading dim ldX (host,
@@ -28,6 +34,15 @@ class AlsSession {
     void set_quiet(bool q) { quiet_ = q; }
     void set_timing(bool on);
     void kernel_ms(double* fit, double* m3, double* it, int* samples);
+    // Switch this session to the nonconvex solver of test.m (before run):
+    // same fit/M1/M2/K2 kernels over X, plus the O / Lambda / Gamma ADMM
+    // chain fused into the fit kernel, ridge 1e-12 + reweighted shrink on A,
+    // errHist/stop/print at the END of the iteration (test.m:62-68).
+    void enable_ncvx(const NcvxParams& p);
+    bool ncvx() const { return ncvx_; }
+    // O returned by test.m: that of iteration k-1 when the stop test broke
+    // the loop at k (:67 before :71), else the last one; column-major shard
+    void get_O(double* O, int64_t ldO);
 
     // --- phase interface (device groups drive these; see api.cpp) -------
     int next_iter();
@@ -36,6 +51,7 @@ class AlsSession {
     void phaseA(int k);    // M1, solve A, apply A, A^TA partial, M2 partial -> red1
     void phaseB(int k);    // solve B, apply B, B^TB, M3 partial -> red2
     void phaseC(int k);    // solve C, apply C, C^TC
+    void phaseEnd(int k);  // ncvx: errHist(k), stop test (after the updates, test.m:62-65)
     void maybe_print(int k);
     double* red0() { return red0_.p; }
     double* red1() { return red1_.p; }
@@ -68,6 +84,9 @@ class AlsSession {
     double acc_fit_ = 0, acc_m3_ = 0, acc_it_ = 0;
     int acc_n_ = 0;
     void harvest_timing();
+    bool ncvx_ = false;
+    NcvxParams np_{};
+    DBuf Oa_, Ob_, Lam_, Gam_;  // ncvx: O double buffer (iteration parity), duals (tile-major)
 };
 
 }  // namespace tritd

@@ -250,7 +250,8 @@ void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t 
 void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, int64_t n2,
                    int64_t n3, int32_t r, int maxIter, double tol, const double* A0,
                    const double* B0, const double* C0, double* A, double* B, double* C,
-                   double* errHist, int32_t* iters) {
+                   double* errHist, int32_t* iters, const NcvxParams* ncvx = nullptr,
+                   double* O = nullptr) {
     DeviceGroup grp(devs, n1);
     const int P = grp.size();
     std::vector<std::unique_ptr<AlsSession>> ss;
@@ -259,6 +260,7 @@ void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, in
         TRITD_HIP(hipSetDevice(devs[p]));
         ss.emplace_back(new AlsSession(devs[p], X + i0, n1, n1, n2, n3, i0, i1, r, maxIter, tol, A0,
                                        B0, C0, nullptr, 0, grp.vst, /*defer_norm=*/true));
+        if (ncvx) ss.back()->enable_ncvx(*ncvx);
     }
     auto each = [&](auto&& f) { DeviceGroup::each(ss, f); };
     grp.reduce(ss, &AlsSession::red0, 2);
@@ -271,17 +273,23 @@ void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, in
         grp.reduce(ss, &AlsSession::red0, 2);
         each([&](AlsSession& s) { s.phaseErr(k); });
         TRITD_HIP(hipSetDevice(devs[0]));
-        ss[0]->maybe_print(k);
+        if (!ncvx) ss[0]->maybe_print(k);
         each([&](AlsSession& s) { s.phaseA(k); });
         grp.reduce(ss, &AlsSession::red1, ss[0]->red1_count());
         each([&](AlsSession& s) { s.phaseB(k); });
         grp.reduce(ss, &AlsSession::red2, ss[0]->red2_count());
         each([&](AlsSession& s) { s.phaseC(k); });
+        each([&](AlsSession& s) { s.phaseEnd(k); });  // ncvx: errHist / stop after the updates
+        if (ncvx) {
+            TRITD_HIP(hipSetDevice(devs[0]));
+            ss[0]->maybe_print(k);
+        }
     }
     int k = 0;
     for (int p = 0; p < P; ++p) {
         TRITD_HIP(hipSetDevice(devs[p]));
         ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, p == 0 ? errHist : nullptr, &k);
+        if (ncvx && O) ss[p]->get_O(O + ss[p]->geom().i0, n1);
     }
     if (iters) *iters = k;
 }
@@ -646,6 +654,35 @@ tritd_status tritd_als_sharded_virtual_f64(const double* X, int64_t n1, int64_t 
         run_als_group(std::vector<int>(nshards, dev), X, n1, n2, n3, r,
                       opts->maxIter < 0 ? 0 : opts->maxIter, opts->tol, A0, B0, C0, A, B, C,
                       errHist, iters);
+    });
+}
+
+tritd_status tritd_ncvx_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t r,
+                           double rho, double lambda, double gamma_A, double epsilon, double p,
+                           double theta, int32_t maxIter, double tol, const double* A0,
+                           const double* B0, const double* C0, double* A, double* B, double* C,
+                           double* O, double* errHist, int32_t* iters, int32_t device) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    return guarded([&] {
+        check_dims(n1, n2, n3, r);
+        need(X, "X"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
+        need(A, "A"); need(B, "B"); need(C, "C"); need(O, "O"); need(errHist, "errHist");
+        if (!(rho != 0.0)) throw Error(TRITD_ERR_ARG, "rho must be non-zero");
+        const NcvxParams np{rho, lambda, gamma_A, epsilon, p, theta};
+        const int mi = maxIter < 0 ? 0 : maxIter;
+        if (device < 0 && g_devices.size() > 1) {
+            run_als_group(g_devices, X, n1, n2, n3, r, mi, tol, A0, B0, C0, A, B, C, errHist, iters,
+                          &np, O);
+            return;
+        }
+        const int dev = pick_device(device < 0 && !g_devices.empty() ? g_devices[0] : device);
+        AlsSession s(dev, X, n1, n1, n2, n3, 0, n1, r, mi, tol, A0, B0, C0, nullptr, 0);
+        s.enable_ncvx(np);
+        s.run(mi);
+        int k = 0;
+        s.get(A, B, C, errHist, &k);
+        s.get_O(O, n1);
+        if (iters) *iters = k;
     });
 }
 

@@ -26,7 +26,10 @@ __device__ __forceinline__ d4 als_mfma4(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int RP>
+// sign() of MATLAB without branches: 1, -1, 0 for +-0, NaN for NaN
+__device__ __forceinline__ double nc_sign(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : x); }
+
+template <int RP, bool NCV>
 __global__ __launch_bounds__(64 * FIT_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_als_fit(AlsFitArgs a) {
     if (*a.stop) return;
@@ -87,11 +90,24 @@ void k_als_fit(AlsFitArgs a) {
     // would make the compiler wait for the prefetch at the copy; k_admm.hip).
     struct Regs {
         d2v x[2];
+        d2v e[NCV ? 3 : 1][2];  // NCV: O, Lam, Gam of the same tile
     };
+    const d2v* Oi2 = reinterpret_cast<const d2v*>(a.O_in);
+    d2v* Oo2 = reinterpret_cast<d2v*>(a.O_out);
+    d2v* L2 = reinterpret_cast<d2v*>(a.Lam);
+    d2v* G2 = reinterpret_cast<d2v*>(a.Gam);
     auto load = [&](int64_t tt, Regs& nx) {
         const int64_t o = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
         nx.x[0] = X2[o];
         nx.x[1] = X2[o + 64];
+        if constexpr (NCV) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                nx.e[0][h] = Oi2[o + 64 * h];
+                nx.e[1][h] = L2[o + 64 * h];
+                nx.e[2][h] = G2[o + 64 * h];
+            }
+        }
     };
     auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
         if (pf) {
@@ -106,10 +122,38 @@ void k_als_fit(AlsFitArgs a) {
         for (int s = 0; s < KS; ++s) lacc = als_mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
         double xr[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            xr[r] = cx.x[r >> 1][r & 1];
-            const double d = xr[r] - lacc[r];  // X(:) - Xhat(:)
-            ss += d * d;
+        for (int r = 0; r < 4; ++r) xr[r] = cx.x[r >> 1][r & 1];
+        if constexpr (NCV) {
+            // test.m:36,44,47,48,62 in MATLAB's operator order (-ffp-contract=off)
+            const int64_t o = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
+            d2v on[2], ln[2], gn[2];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double x = xr[r], L = lacc[r];
+                const double O = cx.e[0][r >> 1][r & 1], Lm = cx.e[1][r >> 1][r & 1],
+                             Gm = cx.e[2][r >> 1][r & 1];
+                const double Y = ((x - O) + a.rho * (L + Lm / a.rho)) / a.onep;
+                const double xy = x - Y;
+                const double z = xy + Gm / a.rho;
+                const double On = nc_sign(z) * fmax(fabs(z) - a.tau, 0.0);
+                const double d = xy - On;
+                on[r >> 1][r & 1] = On;
+                ln[r >> 1][r & 1] = Lm + a.rho * (L - Y);
+                gn[r >> 1][r & 1] = Gm + a.rho * d;
+                ss += d * d;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                Oo2[o + 64 * h] = on[h];
+                L2[o + 64 * h] = ln[h];
+                G2[o + 64 * h] = gn[h];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double d = xr[r] - lacc[r];  // X(:) - Xhat(:)
+                ss += d * d;
+            }
         }
         // W^T(k, ij) += sum_t C^(t,k) X(t, ij): the C/D register r of the X
         // tile (t = t0 + 4r + l>>4, ij = l&15) is directly the B operand
@@ -125,6 +169,9 @@ void k_als_fit(AlsFitArgs a) {
 
     Regs xa, xb;
     xa.x[0] = xa.x[1] = xb.x[0] = xb.x[1] = d2v{0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < (NCV ? 3 : 1); ++q)
+        xa.e[q][0] = xa.e[q][1] = xb.e[q][0] = xb.e[q][1] = d2v{0.0, 0.0};
     load(0, xa);
     stage_load(0);
     stage_store(0);
@@ -166,13 +213,21 @@ int als_fit_grid(const Geom& g) { return (int)cdiv(g.tiles, FIT_WAVES); }
 
 void launch_als_fit(const Geom& g, const AlsFitArgs& a, hipStream_t st) {
     const dim3 grid(als_fit_grid(g)), block(64 * FIT_WAVES);
+#define FIT_CASE(RPV)                                                                  \
+    case RPV:                                                                          \
+        if (a.ncvx)                                                                    \
+            hipLaunchKernelGGL((k_als_fit<RPV, true>), grid, block, 0, st, a);         \
+        else                                                                           \
+            hipLaunchKernelGGL((k_als_fit<RPV, false>), grid, block, 0, st, a);        \
+        break;
     switch (g.RP) {
-        case 16: hipLaunchKernelGGL(k_als_fit<16>, grid, block, 0, st, a); break;
-        case 32: hipLaunchKernelGGL(k_als_fit<32>, grid, block, 0, st, a); break;
-        case 48: hipLaunchKernelGGL(k_als_fit<48>, grid, block, 0, st, a); break;
-        case 64: hipLaunchKernelGGL(k_als_fit<64>, grid, block, 0, st, a); break;
+        FIT_CASE(16)
+        FIT_CASE(32)
+        FIT_CASE(48)
+        FIT_CASE(64)
         default: throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by the ALS fit kernel");
     }
+#undef FIT_CASE
     TRITD_CHECK_LAUNCH();
 }
 
@@ -192,6 +247,33 @@ __global__ void k_als_finish(const double* ss, double Xnorm, int k, double tol, 
 void launch_als_finish(const double* ss, double Xnorm, int k, double tol, double* errHist,
                        int* ctrl, hipStream_t st) {
     hipLaunchKernelGGL(k_als_finish, dim3(1), dim3(1), 0, st, ss, Xnorm, k, tol, errHist, ctrl);
+    TRITD_CHECK_LAUNCH();
+}
+
+// Reweighted shrink of the A update of test.m:82-92 (after the ridge-1e-12
+// solve and apply): W_A = 1./((abs(A1) + epsilon).^(theta - p)) (:86),
+// A1 = sign(A1).*max(abs(A1) - gamma_A.*W_A, 0) (:89, weighted_soft_threshold
+// :97-101); written to Ah and its transposed copy AhT.  Zero pads stay zero.
+__global__ __launch_bounds__(256) void k_ncvx_shrink(double* Ah, double* AhT, int64_t n1p, int RP,
+                                                     double gamma, double eps, double expo,
+                                                     const int* stop) {
+    if (*stop) return;
+    const int64_t n = n1p * RP;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        const double x = Ah[e];
+        const double w = 1.0 / pow(fabs(x) + eps, expo);
+        const double v = nc_sign(x) * fmax(fabs(x) - gamma * w, 0.0);
+        Ah[e] = v;
+        const int64_t i = e / RP, k = e - i * RP;
+        AhT[k * n1p + i] = v;
+    }
+}
+
+void launch_ncvx_shrink(const Geom& g, double* Ah, double* AhT, double gamma, double eps,
+                        double expo, const int* stop, hipStream_t st) {
+    const int64_t n = g.n1p * g.RP;
+    hipLaunchKernelGGL(k_ncvx_shrink, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 2048)),
+                       dim3(256), 0, st, Ah, AhT, g.n1p, g.RP, gamma, eps, expo, stop);
     TRITD_CHECK_LAUNCH();
 }
 

@@ -135,12 +135,23 @@ struct AlsFitArgs {
     double* partial;   // [grid][2]: sum (X - Xhat)^2, 0
     int64_t n1p, n2, n3p, plane, tiles, ntt;
     const int* stop;
+    // nonconvex variant (fast_robust_triple_tensor/test.m:35-48; ncvx != 0):
+    // Y = ((X - O) + rho*(L + Lam/rho))/onep; O' = shrink((X - Y) + Gam/rho, tau);
+    // Lam += rho*(L - Y); Gam += rho*((X - Y) - O'); partial = sum ((X - Y) - O')^2.
+    // O is double-buffered (O_in of iteration k-1, O_out of k), tile-major.
+    int ncvx;
+    const double* O_in;
+    double *O_out, *Lam, *Gam;
+    double rho, tau, onep;
 };
 int als_fit_grid(const Geom& g);
 void launch_als_fit(const Geom& g, const AlsFitArgs& a, hipStream_t st);
 void launch_als_finish(const double* ss, double Xnorm, int k, double tol, double* errHist,
                        int* ctrl, hipStream_t st);
 void launch_tm_to_tx(const Geom& g, const double* src, double* dst, hipStream_t st);
+// test.m:82-92: A1 <- sign(A1).*max(|A1| - gamma*(1./((|A1|+eps).^expo)), 0), into Ah and AhT
+void launch_ncvx_shrink(const Geom& g, double* Ah, double* AhT, double gamma, double eps,
+                        double expo, const int* stop, hipStream_t st);
 
 // ---- driver-side metrics (k_metrics.hip) ------------------------------------
 // evaluate (traffic_triple_comparison.m:194-202): out2 = {sum (X(mask)-gt)^2,

@@ -130,7 +130,8 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (!size3(D, n, &err)) fail("tritd:dims", err);
     const int32_t r = (int32_t)mxGetScalar(prhs[2]);
     tritd_opts o;
-    if (!read_opts(prhs[3], &o, &err)) fail("MATLAB:nonExistentField", err);
+    if (!read_opts(prhs[3], &o, &err))
+        fail(err.rfind("Reference", 0) == 0 ? "MATLAB:nonExistentField" : "tritd:opts", err);
     for (int k = 4; k < 7; ++k) need_double(prhs[k], "initial factor");
     const int64_t R = (int64_t)r * r;
     if ((int64_t)mxGetNumberOfElements(prhs[4]) != n[0] * R ||
@@ -232,6 +233,52 @@ void do_als(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     }
 }
 
+// [A,B,C,O,errHist] = tritd_mex('ncvx', X, r, rho, lambda, gamma_A, epsilon, p, theta,
+//                                maxIter, tol, A0, B0, C0)   (fast_robust_triple_tensor/test.m:1)
+void do_ncvx(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs != 14)
+        fail("tritd:nargin", "usage: tritd_mex('ncvx', X, r, rho, lambda, gamma_A, epsilon, p, "
+                             "theta, maxIter, tol, A0, B0, C0)");
+    need_double(prhs[1], "X");
+    int64_t n[3];
+    std::string err;
+    if (!size3(prhs[1], n, &err)) fail("tritd:dims", err);
+    const int32_t r = (int32_t)mxGetScalar(prhs[2]);
+    double prm[6];
+    for (int q = 0; q < 6; ++q) prm[q] = mxGetScalar(prhs[3 + q]);
+    const int32_t maxIter = (int32_t)mxGetScalar(prhs[9]);
+    const double tol = mxGetScalar(prhs[10]);
+    for (int k = 11; k < 14; ++k) need_double(prhs[k], "initial factor");
+    const int64_t R = (int64_t)r * r;
+    if ((int64_t)mxGetNumberOfElements(prhs[11]) != n[0] * R ||
+        (int64_t)mxGetNumberOfElements(prhs[12]) != R * n[1] ||
+        (int64_t)mxGetNumberOfElements(prhs[13]) != R * n[2])
+        fail("tritd:dims", "A0, B0, C0 must be n1 x r x r, r x n2 x r, r x r x n3");
+    mxArray* A = make3(n[0], r, r);
+    mxArray* B = make3(r, n[1], r);
+    mxArray* C = make3(r, r, n[2]);
+    mxArray* O = make3(n[0], n[1], n[2]);
+    mxArray* eh = mxCreateDoubleMatrix(maxIter > 0 ? maxIter : 0, 1, mxREAL);
+    int32_t k = 0;
+    tritd_set_print_callback(print_line, nullptr);
+    const tritd_status st = tritd_ncvx_f64(
+        mxGetPr(prhs[1]), n[0], n[1], n[2], r, prm[0], prm[1], prm[2], prm[3], prm[4], prm[5],
+        maxIter, tol, mxGetPr(prhs[11]), mxGetPr(prhs[12]), mxGetPr(prhs[13]), mxGetPr(A),
+        mxGetPr(B), mxGetPr(C), mxGetPr(O), maxIter > 0 ? mxGetPr(eh) : nullptr, &k, -1);
+    if (st != TRITD_OK) {
+        for (mxArray* x : {A, B, C, O, eh}) mxDestroyArray(x);
+        fail("tritd:solver", status_msg(st));
+    }
+    mxSetM(eh, (mwSize)k);  // errHist(1:k) on a break (test.m:66); maxIter entries otherwise
+    mxArray* outs[5] = {A, B, C, O, eh};
+    for (int q = 0; q < 5; ++q) {
+        if (q < (nlhs > 0 ? nlhs : 1))
+            plhs[q] = outs[q];
+        else
+            mxDestroyArray(outs[q]);
+    }
+}
+
 void do_devices(int, mxArray*[], int nrhs, const mxArray* prhs[]) {
     if (nrhs != 2) fail("tritd:nargin", "usage: tritd_mex('devices', idx)");
     need_double(prhs[1], "idx");
@@ -325,6 +372,8 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         do_admm(nlhs, plhs, nrhs, prhs);
     else if (c == "als")
         do_als(nlhs, plhs, nrhs, prhs);
+    else if (c == "ncvx")
+        do_ncvx(nlhs, plhs, nrhs, prhs);
     else if (c == "triple_product")
         do_triple_product(nlhs, plhs, nrhs, prhs);
     else if (c == "unfold")

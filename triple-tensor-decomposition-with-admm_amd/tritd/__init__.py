@@ -21,6 +21,7 @@ from .api import (  # noqa: F401
     soft_threshold,
     triple_decomp_ADMM,
     triple_decomp_ADMM_outlier,
+    triple_decomp_ncvx,
     triple_decomp_ALS,
     triple_product,
     unfold,

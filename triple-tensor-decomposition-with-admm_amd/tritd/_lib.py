@@ -101,6 +101,8 @@ SIGNATURES = {
     "tritd_dev_soft_threshold_f64": (C.c_int, [vp, i64, C.c_double, vp, vp]),
     "tritd_dev_triple_product_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp, vp]),
     "tritd_triple_product_qi_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp]),
+    "tritd_ncvx_f64": (C.c_int, [vp, i64, i64, i64, i32] + [C.c_double] * 6
+                       + [i32, C.c_double, vp, vp, vp, vp, vp, vp, vp, vp, C.POINTER(i32), i32]),
     "tritd_dev_triple_product_qi_f64": (C.c_int, [vp, vp, vp, i64, i64, i64, i32, vp, vp]),
 }
 

@@ -5,6 +5,8 @@ the MATLAB file it replaces and runs on the GPU through libtritd.so:
 
     triple_decomp_ADMM(D, r, opts)          fast_robust_triple_tensor/triple_decomp_ADMM.m:1
     triple_decomp_ADMM_outlier(D, r, opts)  alias expected at video_triple_comparison.m:54
+    triple_decomp_ADMM_outlier(X, r, rho, lambda, gamma_A, epsilon, p, theta, maxIter, tol)
+                                            fast_robust_triple_tensor/test.m:1 (nonconvex variant)
     triple_decomp_ALS(X, r, opts)           fast_robust_triple_tensor/triple_decomp_ALS.m:1
     triple_product(A, B, C[, model])        triple_product.m:1 (model='qi': origin_triple_tensor/)
     unfold(X, mode)                         unfold.m:1
@@ -181,7 +183,49 @@ def _admm_f32(D, r, o, opts, A0, B0, C0, device, return_E, return_iters):
 
 
 # the name video_triple_comparison.m:54 calls (unresolvable in the reference)
-triple_decomp_ADMM_outlier = triple_decomp_ADMM
+def triple_decomp_ncvx(X, r, rho, lam, gamma_A, epsilon, p, theta, maxIter, tol, A0=None,
+                       B0=None, C0=None, *, device=-1, return_iters=False):
+    """[A,B,C,O,errHist] of fast_robust_triple_tensor/test.m:1-73 on the GPU
+    (the nonconvex variant): outlier ADMM over
+    Y = X - O with duals Lambda/Gamma fused into the ALS fit kernel, the
+    factors an ALS on X with ridge 1e-12 and the reweighted shrink
+    sign(A1).*max(|A1| - gamma_A./(|A1|+epsilon).^(theta-p), 0) on A (:77-92).
+    The progress line of :63 goes to the printer every iteration.  On the stop
+    test (:65-67) errHist is truncated and O is that of the previous iteration
+    (the reference breaks before O = O_new, :71).  fp64, r <= 8."""
+    X = _fortran(X)
+    n1, n2, n3 = _size3(X)
+    r = int(r)
+    maxIter = int(maxIter)
+    if A0 is None or B0 is None or C0 is None:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r)
+    else:
+        A0, B0, C0 = initial_factors(n1, n2, n3, r, dict(A0=A0, B0=B0, C0=C0))
+    A = np.zeros((n1, r, r), order="F")
+    B = np.zeros((r, n2, r), order="F")
+    Cf = np.zeros((r, r, n3), order="F")
+    O = np.zeros((n1, n2, n3), order="F")
+    errHist = np.zeros(max(maxIter, 1))
+    k = _lib.i32(0)
+    check(lib.tritd_ncvx_f64(_ptr(X), n1, n2, n3, r, float(rho), float(lam), float(gamma_A),
+                             float(epsilon), float(p), float(theta), maxIter, float(tol), _ptr(A0),
+                             _ptr(B0), _ptr(C0), _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(errHist),
+                             C.byref(k), int(device)))
+    out = [A, B, Cf, O, errHist[: k.value].copy()]
+    if return_iters:
+        out.append(k.value)
+    return tuple(out)
+
+
+def triple_decomp_ADMM_outlier(*args, **kw):
+    """The name the video driver calls (video_triple_comparison.m:54).  In the
+    reference it resolves to two different files' internal names: with
+    (D, r, opts) it is the ADMM solver (origin_triple_tensor/triple_decomp_ADMM.m:1,
+    same maths as the fast one), with the 10 positional arguments of
+    fast_robust_triple_tensor/test.m:1 it is the nonconvex variant."""
+    if len(args) >= 10:
+        return triple_decomp_ncvx(*args, **kw)
+    return triple_decomp_ADMM(*args, **kw)
 
 
 def make_als_opts(opts):
@@ -530,6 +574,7 @@ class Comm:
 
 
 __all__ = ["triple_decomp_ADMM", "triple_decomp_ADMM_outlier", "triple_decomp_ALS", "AlsSession",
+           "triple_decomp_ncvx",
            "make_als_opts", "evaluate", "quality_ybz", "triple_product", "unfold",
            "soft_threshold", "buildF", "buildG", "buildH", "Session", "Comm", "TritdError",
            "make_opts", "initial_factors"]
