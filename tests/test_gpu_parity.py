@@ -170,7 +170,8 @@ def test_maxiter_zero_returns_initial_factors(tritd):
 # ---------------------------------------------------------------------------
 # primitives
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("shape", [(12, 10, 8), (30, 30, 30), (65, 3, 130), (1, 7, 1), (128, 64, 2)])
+@pytest.mark.parametrize("shape", [(12, 10, 8), (30, 30, 30), (65, 3, 130), (1, 7, 1), (128, 64, 2),
+                                   (128, 64, 128), (64, 256, 256)])  # last two: k_transpose_tall
 def test_unfold_bit_exact(tritd, orc, shape):
     X = np.asfortranarray(np.random.default_rng(1).standard_normal(shape))
     for mode in (1, 2, 3):
@@ -189,6 +190,10 @@ def test_soft_threshold_bit_exact(tritd, orc):
     for lam in (0.0, 1.8, 1e-4):
         got = tritd.soft_threshold(X, lam)
         np.testing.assert_array_equal(got, orc.soft_threshold(X, lam))
+    # several grid steps of the 8-pair-per-thread kernel, a ragged tail and n odd
+    for n in (2 * 8 * 256 * 3 + 7, 1 << 22):
+        Y = rng.standard_normal(n)
+        np.testing.assert_array_equal(tritd.soft_threshold(Y, 0.7), orc.soft_threshold(Y, 0.7))
 
 
 @pytest.mark.parametrize("n1,n2,n3,r", [(12, 10, 8, 2), (30, 31, 29, 3), (17, 16, 20, 8), (5, 4, 33, 5)])

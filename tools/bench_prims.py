@@ -22,8 +22,9 @@ HBM = 8000.0   # GB/s, MI355X_MICROARCH.md
 F64_MFMA = 78.6  # TF/s dense f64 matrix
 
 
-def timed(fn, reps, stream):
-    fn()
+def timed(fn, reps, stream, warm=3):
+    for _ in range(warm):
+        fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -63,7 +64,7 @@ def main():
         out["kernels"][name] = d
 
     p = lambda t: C.c_void_p(t.data_ptr())
-    for mode in (2, 3):
+    for mode in (2, 3, 2):  # mode 2 again: the first timed kernel of the process ran slow
         ms = timed(lambda: check(lib.tritd_dev_unfold_f64(p(X), n, n, n, mode, p(Y), sp)), a.reps, st)
         rec("unfold_mode%d" % mode, ms, 2 * N * 8)
     ms = timed(lambda: check(lib.tritd_dev_soft_threshold_f64(p(X), N, C.c_double(0.5), p(Y), sp)),

@@ -1,0 +1,6 @@
+set -uo pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "unfold or soft_threshold" > gpurun_out/prim_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/prim_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python3 tools/bench_prims.py > gpurun_out/prims.json 2> gpurun_out/prims.err || exit $?
+cat gpurun_out/prims.json

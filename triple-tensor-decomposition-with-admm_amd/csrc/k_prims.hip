@@ -215,6 +215,10 @@ void launch_pack_factors(const Geom& g, const double* A, const double* B, const 
 // 64 x 64 tile through LDS, 16-byte global accesses on both sides.
 // ---------------------------------------------------------------------------
 constexpr int TT = 64;
+// FULL: every tile is whole and 16-B aligned (checked on the host), so the
+// kernel carries no bounds logic and issues its eight loads back to back
+// (the bounds-checked form ran mode 2 at 512^3 in 0.425 vs 0.342 ms).
+template <bool FULL>
 __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in,
                                                    double* __restrict__ out, int64_t rows,
                                                    int64_t cols) {
@@ -224,19 +228,24 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in
     const double* src = in + b * rows * cols;
     double* dst = out + b * rows * cols;
     const int th = threadIdx.x;
-    const bool full = (r0 + TT <= rows) && (c0 + TT <= cols) && ((rows & 1) == 0) && ((cols & 1) == 0);
     // load: thread -> (c = th/32 + 8m, r = 2*(th%32))
     {
         const int rr = 2 * (th & 31), cc = th >> 5;
+        if constexpr (FULL) {
+            d2v v[8];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int c = cc + 8 * m;
-            const int64_t gc = c0 + c, gr = r0 + rr;
-            if (full) {
-                const double2 v = *reinterpret_cast<const double2*>(src + gc * rows + gr);
-                tile[c][rr] = v.x;
-                tile[c][rr + 1] = v.y;
-            } else {
+            for (int m = 0; m < 8; ++m)
+                v[m] = *reinterpret_cast<const d2v*>(src + (c0 + cc + 8 * m) * rows + r0 + rr);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                tile[cc + 8 * m][rr] = v[m].x;
+                tile[cc + 8 * m][rr + 1] = v[m].y;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int c = cc + 8 * m;
+                const int64_t gc = c0 + c, gr = r0 + rr;
                 tile[c][rr] = (gc < cols && gr < rows) ? src[gc * rows + gr] : 0.0;
                 tile[c][rr + 1] = (gc < cols && gr + 1 < rows) ? src[gc * rows + gr + 1] : 0.0;
             }
@@ -250,8 +259,8 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in
         for (int m = 0; m < 8; ++m) {
             const int r = rr + 8 * m;
             const int64_t gr = r0 + r, gc = c0 + cc;
-            if (full) {
-                *reinterpret_cast<double2*>(dst + gr * cols + gc) = double2{tile[cc][r], tile[cc + 1][r]};
+            if constexpr (FULL) {
+                *reinterpret_cast<d2v*>(dst + gr * cols + gc) = d2v{tile[cc][r], tile[cc + 1][r]};
             } else {
                 if (gr < rows && gc < cols) dst[gr * cols + gc] = tile[cc][r];
                 if (gr < rows && gc + 1 < cols) dst[gr * cols + gc + 1] = tile[cc + 1][r];
@@ -260,11 +269,60 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in
     }
 }
 
+// Tall single transpose (unfold mode 3: rows = n1*n2 >> cols = n3): TR x TC
+// tiles with the column tile fastest in blockIdx.x, so the blocks resident
+// together write whole output rows (cols doubles) instead of TC-wide slivers
+// of rows spread over the whole output, and all global loads issue before
+// the LDS stores.  Measured at 512^3 (tools/prim_stream.hip): 32 x 128 tiles
+// 0.385 ms = 5.58 TB/s vs 0.41 ms for the 64 x 64 row-fastest kernel.
+template <int TR, int TC>
+__global__ __launch_bounds__(256) void k_transpose_tall(const double* __restrict__ in,
+                                                        double* __restrict__ out, int64_t rows,
+                                                        int64_t cols, int64_t nct) {
+    __shared__ double tile[TC][TR + 1];
+    const int64_t ct = blockIdx.x % nct, rt = blockIdx.x / nct;
+    const int64_t r0 = rt * TR, c0 = ct * TC;
+    const int th = threadIdx.x;
+    constexpr int PR = TR / 2, CPP = 256 / PR, ML = TC / CPP;  // loads: column pairs of rows
+    d2v v[ML];
+    const int rp = th % PR, cc = th / PR;
+#pragma unroll
+    for (int m = 0; m < ML; ++m)
+        v[m] = *reinterpret_cast<const d2v*>(in + (c0 + cc + CPP * m) * rows + r0 + 2 * rp);
+#pragma unroll
+    for (int m = 0; m < ML; ++m) {
+        tile[cc + CPP * m][2 * rp] = v[m].x;
+        tile[cc + CPP * m][2 * rp + 1] = v[m].y;
+    }
+    __syncthreads();
+    constexpr int PC = TC / 2, RPP = 256 / PC, MS = TR / RPP;  // stores: row pairs of columns
+    const int cp = th % PC, rr = th / PC;
+#pragma unroll
+    for (int m = 0; m < MS; ++m) {
+        const int r = rr + RPP * m;
+        *reinterpret_cast<d2v*>(out + (r0 + r) * cols + c0 + 2 * cp) =
+            d2v{tile[2 * cp][r], tile[2 * cp + 1][r]};
+    }
+}
+
 void launch_transpose_batched(const double* in, double* out, int64_t rows, int64_t cols,
                               int64_t batch, hipStream_t st) {
     if (batch > 65535) throw Error(TRITD_ERR_ARG, "transpose batch too large");
+    constexpr int TR = 32, TC = 128;
+    if (batch == 1 && rows % TR == 0 && cols % TC == 0 && rows >= 64 * cols &&
+        (((uintptr_t)in | (uintptr_t)out) & 15) == 0 && (rows / TR) * (cols / TC) < (1LL << 31)) {
+        const int64_t nct = cols / TC;
+        hipLaunchKernelGGL((k_transpose_tall<TR, TC>), dim3((unsigned)((rows / TR) * nct)), dim3(256),
+                           0, st, in, out, rows, cols, nct);
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     const dim3 grid((unsigned)cdiv(rows, TT), (unsigned)cdiv(cols, TT), (unsigned)batch);
-    hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, st, in, out, rows, cols);
+    const bool full = rows % TT == 0 && cols % TT == 0 && (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    if (full)
+        hipLaunchKernelGGL(k_transpose<true>, grid, dim3(256), 0, st, in, out, rows, cols);
+    else
+        hipLaunchKernelGGL(k_transpose<false>, grid, dim3(256), 0, st, in, out, rows, cols);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -276,26 +334,40 @@ __device__ __forceinline__ double st1(double x, double lam) {
     return s * fmax(fabs(x) - lam, 0.0);
 }
 
+// Eight 16-B nontemporal loads per thread issued before the first store, a
+// block owning 8 * 256 consecutive pairs per step (tools/prim_stream.hip at
+// 512^3: 0.339 ms = 6.33 TB/s, the plain-copy ceiling of the chip, vs 0.39-0.41 ms
+// for one load per grid-stride step).
+constexpr int ST_U = 8;
 __global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict__ X, int64_t n,
                                                         double lam, double* __restrict__ Y) {
     const int64_t n2 = n >> 1;
-    const int64_t stride = (int64_t)gridDim.x * 256;
     const d2v* X2 = reinterpret_cast<const d2v*>(X);
     d2v* Y2 = reinterpret_cast<d2v*>(Y);
-    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n2; e += stride) {
-        const d2v v = __builtin_nontemporal_load(X2 + e);
-        d2v o;
-        o.x = st1(v.x, lam);
-        o.y = st1(v.y, lam);
-        __builtin_nontemporal_store(o, Y2 + e);
+    for (int64_t base = (int64_t)blockIdx.x * ST_U * 256; base < n2;
+         base += (int64_t)gridDim.x * ST_U * 256) {
+        d2v v[ST_U];
+#pragma unroll
+        for (int u = 0; u < ST_U; ++u) {
+            const int64_t e = base + u * 256 + threadIdx.x;
+            v[u] = e < n2 ? __builtin_nontemporal_load(X2 + e) : d2v{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < ST_U; ++u) {
+            const int64_t e = base + u * 256 + threadIdx.x;
+            d2v o;
+            o.x = st1(v[u].x, lam);
+            o.y = st1(v[u].y, lam);
+            if (e < n2) __builtin_nontemporal_store(o, Y2 + e);
+        }
     }
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) Y[n - 1] = st1(X[n - 1], lam);
 }
 
 void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hipStream_t st) {
     if (((uintptr_t)X | (uintptr_t)Y) & 15) throw Error(TRITD_ERR_ARG, "soft_threshold: 16-B alignment");
-    int64_t blocks = cdiv(n / 2, 256 * 4);
-    if (blocks > 8192) blocks = 8192;
+    int64_t blocks = cdiv(n / 2, 256 * ST_U);
+    if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_soft_threshold, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
     TRITD_CHECK_LAUNCH();
