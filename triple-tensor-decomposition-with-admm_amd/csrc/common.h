@@ -94,6 +94,7 @@ struct IterScalars {
     double den;          // muL + muO             (:43)
     double invL_next;    // 1/muL of the next iteration (fused T formation, :33)
     double muO_prev;     // muO of the previous iteration (derived Y_O, k_admm.hip)
+    double rden;         // 1/den, correctly rounded (K5's division by den, k_admm.hip)
 };
 
 // first double of tile (g, tt) in the tile-major layout

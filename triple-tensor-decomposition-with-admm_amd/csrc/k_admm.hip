@@ -50,6 +50,21 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_NT
 #define K5_NT 0  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores
 #endif
+#ifndef K5_FASTDIV
+#define K5_FASTDIV 1
+#endif
+#ifndef K5_SWID
+#define K5_SWID 1
+#endif
+#ifndef K5_IBAL
+#define K5_IBAL 1
+#endif
+#ifndef K5_KRLDS
+#define K5_KRLDS 0
+#endif
+#ifndef K5_LSPLIT
+#define K5_LSPLIT 1
+#endif
 #ifndef K5_EXP
 #define K5_EXP 0  // timing experiments only (tools/): drop parts of the t-tile work
 #endif
@@ -101,9 +116,19 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ bool ce_is_dense(double sv) {
-    return (ce_word(sv, 0) & ce_word(sv, 1) & ce_word(sv, 2) & ce_word(sv, 3)) == ~0ull;
+// bit `lane` of a wave-uniform mask: the mask itself as the lane condition
+// (one v_cndmask per use instead of a 64-bit shift, and and compare)
+__device__ __forceinline__ bool lane_bit(uint64_t m, int lane) {
+#if K5_IBAL
+    (void)lane;
+    return __builtin_amdgcn_inverse_ballot_w64(m);
+#else
+    return (m >> lane) & 1;
+#endif
 }
+// A dense (overflowed) tile has all four mask words set; a stored tile has at
+// most CE_CAP < 64 nonzeros, so mask word 0 alone decides (2 readlanes, not 8)
+__device__ __forceinline__ bool ce_is_dense(double sv) { return ce_word(sv, 0) == ~0ull; }
 // This lane's 4 elements (register order r = 2p+q) from its slot double sv
 // (lane l holds slot word l & 31).  Returns true for a dense (overflowed)
 // tile, whose values are in E instead.
@@ -118,10 +143,10 @@ __device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
         const int src = (pre + lanes_below(m[w])) & 63;
         const int vlo = __builtin_amdgcn_ds_bpermute(src << 2, svlo);
         const int vhi = __builtin_amdgcn_ds_bpermute(src << 2, svhi);
-        e[w] = ((m[w] >> lane) & 1) ? __hiloint2double(vhi, vlo) : 0.0;
+        e[w] = lane_bit(m[w], lane) ? __hiloint2double(vhi, vlo) : 0.0;
         pre += __builtin_popcountll(m[w]);
     }
-    return (m[0] & m[1] & m[2] & m[3]) == ~0ull;
+    return m[0] == ~0ull;  // ce_is_dense
 }
 // Store this lane's 4 elements of E (register order) as the tile's slot at
 // CE + sb, or densely into E2 at d2v offset o when they do not fit.  cs: the
@@ -150,7 +175,7 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
     for (int w = 0; w < 4; ++w) {
         // (a dense tile's image is not used: its values go to the junk area,
         // they would index past the scratch)
-        const int bit = dense ? 0 : (int)((nz[w] >> lane) & 1);
+        const int bit = (!dense && lane_bit(nz[w], lane)) ? 1 : 0;
         const int at = pre + lanes_below(nz[w]), away = 32 + lane;
         cs[away + ((at - away) & -bit)] = En[w];
         pre += __builtin_popcountll(nz[w]);
@@ -185,7 +210,9 @@ void k5_fused(K5Args a) {
     constexpr int MT = RP / 16;  // k-tiles of W
     constexpr int LDC = RP + 16; // row stride of the [t][k] C^ slice (2*LDC = 32 mod 64: no bank conflicts)
     const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    // wave-uniform in SGPRs: every tile base below becomes scalar address math
+    // (K5 is VALU-issue-bound)
+    const int wid = K5_SWID ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6);
     const int il = lane & 15;
     const int tg = lane >> 4;
     const int64_t tile = (int64_t)blockIdx.x * K5_WAVES + wid;
@@ -242,6 +269,21 @@ void k5_fused(K5Args a) {
         stage_store(buf);
     };
 
+#if K5_KRLDS
+    // the Khatri-Rao operand lives in LDS (16 doubles per lane, 8 KB per wave):
+    // 32 VGPRs fewer for the t-walk (K5 runs at the 256-VGPR, 2-wave limit)
+    __shared__ double krm[K5_WAVES][KS * 64];
+    double* krs = krm[wid];
+    if (!PRO) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + tg;
+            krs[s * 64 + lane] =
+                active ? a.Ah[j * a.ahj + i * RP + k] * a.Bh[j * a.bhj + k] : 0.0;  // CP or Qi (kernels.h)
+        }
+    }
+#define KR(s) krs[(s) * 64 + lane]
+#else
     double kr[KS];
     if (!PRO) {
 #pragma unroll
@@ -250,6 +292,8 @@ void k5_fused(K5Args a) {
             kr[s] = active ? a.Ah[j * a.ahj + i * RP + k] * a.Bh[j * a.bhj + k] : 0.0;  // CP or Qi (kernels.h)
         }
     }
+#define KR(s) kr[s]
+#endif
     d4 wacc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) wacc[m] = d4{0.0, 0.0, 0.0, 0.0};
@@ -367,9 +411,25 @@ void k5_fused(K5Args a) {
             }
         } else {
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
+#if K5_LSPLIT > 1
+            // K5_LSPLIT independent accumulation chains over the K-steps, summed
+            // in a fixed order (the dependent 16-MFMA chain paces one wave)
+            {
+                d4 lp[K5_LSPLIT];
+#pragma unroll
+                for (int c = 0; c < K5_LSPLIT; ++c) lp[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s = 0; s < KS; ++s)
+                    lp[s % K5_LSPLIT] = mfma4(cT[(4 * s + tg) * 16 + il], KR(s), lp[s % K5_LSPLIT]);
+                lacc = lp[0];
+#pragma unroll
+                for (int c = 1; c < K5_LSPLIT; ++c) lacc = lacc + lp[c];
+            }
+#else
             if (!(K5_EXP & 1))
 #pragma unroll
-                for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
+                for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], KR(s), lacc);
+#endif
             double En[4];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
@@ -383,7 +443,18 @@ void k5_fused(K5Args a) {
                     const double L = lacc[r];
                     const double R1 = (d - L) + sc.invL * yl;               // :41
                     const double R2 = e - sc.invO * yo;                     // :42
+#if K5_FASTDIV
+                    // x/den as a reciprocal product with one exact-residual
+                    // correction (Markstein: q0 = x*(1/den), r = x - q0*den by
+                    // FMA, q = q0 + r*(1/den)); the quotient MATLAB's division
+                    // rounds to, in 3 VALU ops instead of the ~11 of the
+                    // scaled IEEE sequence (K5 is VALU-issue-bound)
+                    const double Onum = sc.muL * R1 + sc.muO * R2;
+                    const double q0 = Onum * sc.rden;
+                    const double On = fma(fma(-q0, sc.den, Onum), sc.rden, q0);  // :43
+#else
                     const double On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
+#endif
                     const double R3 = On + sc.invO * yo;                    // :46
                     const double Ev = matlab_sign(R3) * fmax(fabs(R3) - sc.thr, 0.0);  // :47
                     const double rL = (d - L) - On;                         // :50
@@ -391,8 +462,13 @@ void k5_fused(K5Args a) {
                     const double YLn = yl + sc.muL * rL;                    // :52
                     const double YOn = yo + sc.muO * rO;                    // :53
                     const double Tn = (d - On) + sc.invL_next * YLn;        // :33 (k+1)
+#if K5_FASTDIV
+                    ssL = fma(rL, rL, ssL);  // norm sums: our own order anyway
+                    ssO = fma(rO, rO, ssO);
+#else
                     ssL += rL * rL;
                     ssO += rO * rO;
+#endif
                     En[r] = Ev;
                     YLn2[q] = YLn;
                     YOn2[q] = YOn;

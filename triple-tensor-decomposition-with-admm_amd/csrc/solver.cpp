@@ -303,6 +303,7 @@ IterScalars Session::scalars(int k) const {
     s.invO = 1.0 / s.muO;
     s.thr = o_.lambda / s.muO;
     s.den = s.muL + s.muO;
+    s.rden = 1.0 / s.den;
     s.invL_next = 1.0 / mu_[(size_t)k];
     s.muO_prev = k >= 2 ? mu_[(size_t)k - 2] : 0.0;  // E^(0) = E^(-1) = 0: any value
     return s;
