@@ -56,6 +56,9 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_SWID
 #define K5_SWID 1
 #endif
+#ifndef K5_CSIGN
+#define K5_CSIGN 1
+#endif
 #ifndef K5_IBAL
 #define K5_IBAL 1
 #endif
@@ -456,7 +459,15 @@ void k5_fused(K5Args a) {
                     const double On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
 #endif
                     const double R3 = On + sc.invO * yo;                    // :46
+#if K5_CSIGN
+                    // sign(R3).*max(abs(R3)-thr,0) as copysign (thr > 0): equal
+                    // values (a zero may come out as -0), NaN kept; 7 VALU ops
+                    // instead of 10
+                    double Ev = __builtin_copysign(fmax(fabs(R3) - sc.thr, 0.0), R3);  // :47
+                    Ev = (R3 != R3) ? R3 : Ev;
+#else
                     const double Ev = matlab_sign(R3) * fmax(fabs(R3) - sc.thr, 0.0);  // :47
+#endif
                     const double rL = (d - L) - On;                         // :50
                     const double rO = On - Ev;                              // :51
                     const double YLn = yl + sc.muL * rL;                    // :52

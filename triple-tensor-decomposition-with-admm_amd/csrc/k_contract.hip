@@ -25,19 +25,25 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
 }
 
 // ---------------------------------------------------------------------------
-// M1(i,k) = sum_j Wk[k][j*n1p + i] * Bh[j][k]; block = 64 rows x 4 j-slices
+// M1(i,k) = sum_j Wk[k][j*n1p + i] * Bh[j][k]; block = 64 rows x M1_WAVES
+// j-slices (j = w mod M1_WAVES), 8 independent load/FMA chains per lane,
+// fixed-order LDS sum of the slices.  16 slices: each wave issues ~n2/128
+// batches of 8 loads, so a 64-row shard (8 GPUs at n1 = 512: 64 blocks) is
+// not latency-bound on a few long per-wave chains.
 // (A j-split over more workgroups for 64-row shards, joined by a last-arriver
 // ticket, cost more than it saved: the device-scope fences it needs write
 // back and invalidate L2 on gfx950 and slowed every following kernel.)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_m1(const double* __restrict__ Wk,
-                                            const double* __restrict__ Bh, double* M1,
-                                            int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                            const int* stop) {
+constexpr int M1_WAVES = 16;
+__global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__ Wk,
+                                                      const double* __restrict__ Bh, double* M1,
+                                                      int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                                      const int* stop) {
     if (*stop) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * 64 + lane;
     const int k = blockIdx.y;
+    constexpr int JS = M1_WAVES;
     double acc[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc[u] = 0.0;
@@ -45,22 +51,27 @@ __global__ __launch_bounds__(256) void k_m1(const double* __restrict__ Wk,
         const double* wp = Wk + (int64_t)k * plane + i;
         const double* bp = Bh + k;
         int64_t j = w;
-        for (; j + 28 < n2; j += 32) {  // 8 independent chains, j = w + 4u
+        for (; j + 7 * JS < n2; j += 8 * JS) {  // 8 independent chains, j = w + JS*u
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] = fma(wp[(j + 4 * u) * n1p], bp[(j + 4 * u) * RP], acc[u]);
+            for (int u = 0; u < 8; ++u) acc[u] = fma(wp[(j + JS * u) * n1p], bp[(j + JS * u) * RP], acc[u]);
         }
-        for (; j < n2; j += 4) acc[0] = fma(wp[j * n1p], bp[j * RP], acc[0]);
+        for (; j < n2; j += JS) acc[0] = fma(wp[j * n1p], bp[j * RP], acc[0]);
     }
-    __shared__ double red[4][64];
+    __shared__ double red[JS][64];
     red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     __syncthreads();
-    if (w == 0 && i < n1p) M1[i * RP + k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (w == 0 && i < n1p) {
+        double t = red[0][lane];
+#pragma unroll
+        for (int q = 1; q < JS; ++q) t += red[q][lane];
+        M1[i * RP + k] = t;
+    }
 }
 
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
                hipStream_t st) {
-    hipLaunchKernelGGL(k_m1, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(256), 0, st, Wk, Bh, M1,
-                       g.n1p, g.n2, g.plane, g.RP, stop);
+    hipLaunchKernelGGL(k_m1, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(64 * M1_WAVES), 0, st, Wk,
+                       Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 

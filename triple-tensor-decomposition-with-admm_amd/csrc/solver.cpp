@@ -91,6 +91,10 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         // its off-critical-path Grams and solves on the side stream
         const char* dy = std::getenv("TRITD_DY");
         dy_ = !f32_ && !(dy && std::atoi(dy) == 0);
+        const char* gm = std::getenv("TRITD_GRAM_MAIN");      // overlapped (1-GPU) schedule
+        gram_main_ = gm ? std::atoi(gm) : 0;
+        const char* gms = std::getenv("TRITD_GRAM_MAIN_SH");  // sharded schedule
+        gram_main_sh_ = gms ? std::atoi(gms) : 0;
         const char* sh = std::getenv("TRITD_SHOV");
         shov_ = comm != nullptr && comm->comm != nullptr && shared_stream == nullptr &&
                 !(sh && std::atoi(sh) == 0);
@@ -566,22 +570,26 @@ void Session::iterate_overlapped(int k) {
     // main: M1 -> apply A -> M2 -> apply B -> K2 -> apply C -> K5 -> norms/finish
     // side: Gram A -> solve B | Gram B -> solve C | Gram C -> solve A(k+1)
     hipStream_t gs = (ovmode_ >= 3) ? side_ : st_;
+    // per-Gram placement (gram_main_ bit 0: A^TA, 1: B^TB, 2: C^TC on the main
+    // stream): a Gram beside K2/K5 is starved of memory bandwidth (6 us alone,
+    // 50-330 us beside them) and its solve then lands late
+    auto gsel = [&](int bit) { return (gram_main_ >> bit) & 1 ? st_ : gs; };
     do_m1();
     TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
     do_apply_A(GinvA_.p);
-    if (gs == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    if (gsel(0) == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evAtA_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
-    if (gs == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
+    if (gsel(0) == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
     solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, side_);
     TRITD_HIP(hipEventRecord(evSB_, side_));
     do_m2(M2);
     TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
     do_apply_B(M2, GinvB_.p);
-    if (gs == st_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    if (gsel(1) == st_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
-    if (gs == side_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    if (gsel(1) == side_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
@@ -589,10 +597,10 @@ void Session::iterate_overlapped(int k) {
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     do_apply_C(GinvC_.p);
-    if (gs == st_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    if (gsel(2) == st_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-    if (gs == side_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    if (gsel(2) == side_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/true);
@@ -618,9 +626,10 @@ void Session::iterate_sharded(int k) {
     allreduce(red1_.p, red1_count());
     solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
     do_apply_B(M2, GinvB_.p);
+    if (gram_main_sh_ & 2) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
-    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    if (!(gram_main_sh_ & 2)) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
@@ -629,9 +638,10 @@ void Session::iterate_sharded(int k) {
     allreduce(red2_.p, red2_count());
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     do_apply_C(GinvC_.p);
+    if (gram_main_sh_ & 4) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    if (!(gram_main_sh_ & 4)) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/false);

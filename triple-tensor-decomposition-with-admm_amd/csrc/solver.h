@@ -103,6 +103,7 @@ class Session {
     void launch_k5_full(int k, bool fused_finish);
     bool overlap_ = false;
     int ovmode_ = 2;
+    int gram_main_ = 0, gram_main_sh_ = 0;  // Grams on the main stream (bit 0 A, 1 B, 2 C)
     int rot_ = 1;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
