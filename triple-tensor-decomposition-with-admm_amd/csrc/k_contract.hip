@@ -27,14 +27,14 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
 // ---------------------------------------------------------------------------
 // M1(i,k) = sum_j Wk[k][j*n1p + i] * Bh[j][k]; block = 64 rows x M1_WAVES
 // j-slices (j = w mod M1_WAVES), 8 independent load/FMA chains per lane,
-// fixed-order LDS sum of the slices.  16 slices: each wave issues ~n2/128
-// batches of 8 loads, so a 64-row shard (8 GPUs at n1 = 512: 64 blocks) is
-// not latency-bound on a few long per-wave chains.
+// fixed-order LDS sum of the slices.  16 slices for short shards: each wave
+// issues ~n2/128 batches of 8 loads, so a 64-row shard (8 GPUs at n1 = 512:
+// 64 blocks) is not latency-bound on a few long per-wave chains.
 // (A j-split over more workgroups for 64-row shards, joined by a last-arriver
 // ticket, cost more than it saved: the device-scope fences it needs write
 // back and invalidate L2 on gfx950 and slowed every following kernel.)
 // ---------------------------------------------------------------------------
-constexpr int M1_WAVES = 16;
+template <int M1_WAVES>
 __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__ Wk,
                                                       const double* __restrict__ Bh, double* M1,
                                                       int64_t n1p, int64_t n2, int64_t plane, int RP,
@@ -70,8 +70,15 @@ __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__
 
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
                hipStream_t st) {
-    hipLaunchKernelGGL(k_m1, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(64 * M1_WAVES), 0, st, Wk,
-                       Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
+    // 4 slices when the row blocks alone fill the chip (512 rows: 36 vs 39 us
+    // with 16), 16 for short shards (64 rows: 64 blocks)
+    const dim3 grid((unsigned)cdiv(g.n1p, 64), g.RP);
+    if (g.n1p >= 256)
+        hipLaunchKernelGGL(k_m1<4>, grid, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
+                           g.RP, stop);
+    else
+        hipLaunchKernelGGL(k_m1<16>, grid, dim3(64 * 16), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
+                           g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 
