@@ -154,6 +154,10 @@ tritd_status tritd_session_rre_parts_f32(tritd_session* s, const float* dX, int6
                                          double* num, double* den);
 /* Kernel-level timing of the dominant kernels over the last run (ms per
  * launch, HIP events on the session stream; 0 when timing is disabled). */
+/* enable: 0 off; TRITD_TIMING_ALL (1): per-iteration events around the
+ * iteration, K2 and K5; TRITD_TIMING_K5 (2): around K5 only (each event
+ * record is a stream marker that widens the next kernel boundary by µs) */
+enum { TRITD_TIMING_ALL = 1, TRITD_TIMING_K5 = 2 };
 tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable);
 tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, double* mode3_ms,
                                      double* iteration_ms, int32_t* samples);

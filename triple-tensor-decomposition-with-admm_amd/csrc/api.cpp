@@ -491,7 +491,8 @@ tritd_status tritd_session_rre_parts_f32(tritd_session* s, const float* dX, int6
 tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable) {
     return guarded([&] {
         need(s, "session");
-        reinterpret_cast<Session*>(s)->set_timing(enable != 0);
+        if (enable < 0 || enable > TRITD_TIMING_K5) throw Error(TRITD_ERR_ARG, "timing level 0..2");
+        reinterpret_cast<Session*>(s)->set_timing(enable);
     });
 }
 

@@ -253,7 +253,11 @@ __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ pa
 // waves per t-block (multiple of 4): about two waves per SIMD in total
 int m3_split(const Geom& g) {
     const int64_t ntb = cdiv(g.ntt, 4);
-    int64_t S = 2048 / ntb;
+    static const int64_t waves = [] {  // total waves (TRITD_M3_WAVES: experiments)
+        const char* e = std::getenv("TRITD_M3_WAVES");
+        return e ? (int64_t)std::atoll(e) : (int64_t)2048;
+    }();
+    int64_t S = waves / ntb;
     if (S > g.tiles) S = g.tiles;
     S = (S + 3) / 4 * 4;
     if (S < 4) S = 4;

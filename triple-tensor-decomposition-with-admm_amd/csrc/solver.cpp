@@ -463,9 +463,9 @@ void Session::phaseB(int k) {
     solve(1, AtA, CtC_.p, o_.lambda2, Ginv_.p, st_);
     do_apply_B(M2, Ginv_.p);
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    mark(1);
     do_m3();
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+    mark(2);
 }
 
 void Session::phaseC(int k) {
@@ -547,9 +547,9 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
 }
 
 void Session::launch_k5_full(int k, bool fused_finish) {
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
+    mark(3);
     launch_k5_any(k, /*prologue=*/false);
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 2], st_));
+    mark(4);
     if (fused_finish)  // single GPU: no all-reduce between the norm sums and the stop test
         launch_reduce_finish(k5part_.p, k5_grid(g_), normD_, k, o_.tol, errHist_.p, errL_.p,
                              errO_.p, ctrl_, f32_, st_);
@@ -592,9 +592,9 @@ void Session::iterate_overlapped(int k) {
     if (gsel(1) == side_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    mark(1);
     do_m3();
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+    mark(2);
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     do_apply_C(GinvC_.p);
     if (gsel(2) == st_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
@@ -632,9 +632,9 @@ void Session::iterate_sharded(int k) {
     if (!(gram_main_sh_ & 2)) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 5], st_));
+    mark(1);
     do_m3();
-    if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 4], st_));
+    mark(2);
     allreduce(red2_.p, red2_count());
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     do_apply_C(GinvC_.p);
@@ -674,13 +674,16 @@ void Session::run(int iters) {
         const int k = next_iter();
         if (!k) break;
         if (timing_) {
+            // slots: 0 iteration start, 1/2 K2, 3/4 K5, 5 iteration end; at
+            // TRITD_TIMING_K5 only 3/4 exist (each record is a stream marker
+            // that widens the gap to the next kernel by several us)
             for (int e = 0; e < 6; ++e) {
-                hipEvent_t ev;
-                TRITD_HIP(hipEventCreate(&ev));
+                hipEvent_t ev = nullptr;
+                if (timing_ == TRITD_TIMING_ALL || e == 3 || e == 4) TRITD_HIP(hipEventCreate(&ev));
                 ev_.push_back(ev);
             }
             ev_iter_.push_back(k);
-            TRITD_HIP(hipEventRecord(ev_[ev_.size() - 6], st_));
+            mark(0);
         }
         if (overlap_) {
             iterate_overlapped(k);
@@ -695,7 +698,7 @@ void Session::run(int iters) {
             allreduce(red3_.p, 2);
             phaseD(k);
         }
-        if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 1], st_));
+        mark(5);
         maybe_print(k);
     }
 }
@@ -703,15 +706,16 @@ void Session::run(int iters) {
 void Session::harvest_timing() {
     for (size_t b = 0; b + 6 <= ev_.size(); b += 6) {
         float it = 0, m3 = 0, k5 = 0;
-        TRITD_HIP(hipEventElapsedTime(&it, ev_[b], ev_[b + 5]));
-        TRITD_HIP(hipEventElapsedTime(&m3, ev_[b + 1], ev_[b + 2]));
+        if (ev_[b]) TRITD_HIP(hipEventElapsedTime(&it, ev_[b], ev_[b + 5]));
+        if (ev_[b + 1]) TRITD_HIP(hipEventElapsedTime(&m3, ev_[b + 1], ev_[b + 2]));
         TRITD_HIP(hipEventElapsedTime(&k5, ev_[b + 3], ev_[b + 4]));
         acc_it_ += it;
         acc_m3_ += m3;
         acc_k5_ += k5;
         ++acc_n_;
     }
-    for (auto e : ev_) (void)hipEventDestroy(e);
+    for (auto e : ev_)
+        if (e) (void)hipEventDestroy(e);
     ev_.clear();
     ev_iter_.clear();
 }
@@ -727,8 +731,14 @@ void Session::sync(int* done, int* stopped) {
     if (stopped) *stopped = ctrl[0];
 }
 
-void Session::set_timing(bool on) {
-    timing_ = on;
+void Session::mark(int slot) {
+    if (!timing_) return;
+    hipEvent_t e = ev_[ev_.size() - 6 + slot];
+    if (e) TRITD_HIP(hipEventRecord(e, st_));
+}
+
+void Session::set_timing(int level) {
+    timing_ = level;
     acc_k5_ = acc_m3_ = acc_it_ = 0;
     acc_n_ = 0;
 }

@@ -66,7 +66,7 @@ class Session {
         *dense_streams = dy_ ? 4 : 6;
         *slot_accesses = dy_ ? 3 : 2;
     }
-    void set_timing(bool on);
+    void set_timing(int level);  // 0 off, TRITD_TIMING_ALL, TRITD_TIMING_K5
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
     const std::vector<double>& probe_ms() const { return probe_ms_; }
     int probe_pick() const { return probe_pick_; }
@@ -166,7 +166,8 @@ class Session {
         return reinterpret_cast<unsigned long long*>(ctrl_ + 4);
     }
 
-    bool timing_ = false;
+    int timing_ = 0;
+    void mark(int slot);  // record timing event `slot` of this iteration (if it exists)
     std::vector<hipEvent_t> ev_;  // per timed iteration: 6 events
     std::vector<int> ev_iter_;
     double acc_k5_ = 0, acc_m3_ = 0, acc_it_ = 0;

@@ -466,7 +466,10 @@ class Session:
         return a.value, b.value
 
     def set_timing(self, on=True):
-        check(lib.tritd_session_set_timing(self._s, int(bool(on))))
+        """on: False/0 off, True/1 events around the iteration, K2 and K5,
+        "k5"/2 around K5 only (fewer stream markers inside a timed region)."""
+        level = 2 if on == "k5" else int(on)
+        check(lib.tritd_session_set_timing(self._s, level))
 
     def kernel_ms(self):
         a, b, c = C.c_double(0), C.c_double(0), C.c_double(0)
