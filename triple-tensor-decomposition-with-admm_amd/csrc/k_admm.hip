@@ -56,6 +56,9 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_SWID
 #define K5_SWID 1
 #endif
+#ifndef K5_SMASK
+#define K5_SMASK 0
+#endif
 #ifndef K5_CSIGN
 #define K5_CSIGN 1
 #endif
@@ -115,6 +118,14 @@ __device__ __forceinline__ uint64_t ce_word(double sv, int w) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(__double2hiint(sv), w);
     return ((uint64_t)hi << 32) | lo;
 }
+// Mask word w of the compact-E slot at `slot` through the scalar cache (read
+// only: a uniform address in the constant address space becomes s_load; the
+// kernel later overwrites E^(k-1)'s slot by vector stores but never reads it
+// again, and the scalar cache is invalidated at every kernel start)
+__device__ __forceinline__ uint64_t smask(const double* slot, int w) {
+    typedef const __attribute__((address_space(4))) uint64_t cu64;
+    return ((cu64*)(slot))[w];
+}
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -135,10 +146,17 @@ __device__ __forceinline__ bool ce_is_dense(double sv) { return ce_word(sv, 0) =
 // This lane's 4 elements (register order r = 2p+q) from its slot double sv
 // (lane l holds slot word l & 31).  Returns true for a dense (overflowed)
 // tile, whose values are in E instead.
+__device__ __forceinline__ bool ce_decode_m(double sv, int lane, const uint64_t (&m)[4],
+                                            double (&e)[4]);
 __device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
     uint64_t m[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) m[w] = ce_word(sv, w);
+    return ce_decode_m(sv, lane, m, e);
+}
+// the same with the slot's four mask words already in SGPRs
+__device__ __forceinline__ bool ce_decode_m(double sv, int lane, const uint64_t (&m)[4],
+                                            double (&e)[4]) {
     const int svlo = __double2loint(sv), svhi = __double2hiint(sv);
     int pre = 4;
 #pragma unroll
@@ -369,8 +387,16 @@ void k5_fused(K5Args a) {
         // prefetch first; it only needs tile tt+1's dense flag, whose slot
         // arrived with the batch of this tile
         if (pf) {
+#if K5_SMASK
+            // mask word 0 of tile tt+1's slots by scalar loads (uniform address;
+            // the slot lines are in L2 since the vector slot load of a step ago)
+            const int64_t sn = (tm_tile_base(tile, phys(tt + 1), ntt) >> 8) * CE_SLOT;
+            const bool dn1 = PRO ? false : smask(a.CE + sn, 0) == ~0ull;
+            const bool dnp1 = (PRO || !DY) ? false : smask(a.CEp + sn, 0) == ~0ull;
+#else
             const bool dn1 = PRO ? false : ce_is_dense(nx.ce);
             const bool dnp1 = (PRO || !DY) ? false : ce_is_dense(nx.cep);
+#endif
             stage_load(tt + 1);
             load(tt + 1, nx);
             // keep the prefetch ahead of the compute: the scheduler otherwise
@@ -385,13 +411,28 @@ void k5_fused(K5Args a) {
         }
         double ev[4], evp[4];
         if (!PRO) {
+#if K5_SMASK
+            const int64_t sc0 = (tb >> 8) * CE_SLOT;
+            uint64_t mk[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) mk[w] = smask(a.CE + sc0, w);
+            const bool dn = ce_decode_m(cx.ce, lane, mk, ev);
+#else
             const bool dn = ce_decode(cx.ce, lane, ev);
+#endif
             ev[0] = dn ? cx.ed[0][0] : ev[0];
             ev[1] = dn ? cx.ed[0][1] : ev[1];
             ev[2] = dn ? cx.ed[1][0] : ev[2];
             ev[3] = dn ? cx.ed[1][1] : ev[3];
             if (DY) {
+#if K5_SMASK
+                uint64_t mp[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) mp[w] = smask(a.CEp + sc0, w);
+                const bool dp = ce_decode_m(cx.cep, lane, mp, evp);
+#else
                 const bool dp = ce_decode(cx.cep, lane, evp);
+#endif
                 evp[0] = dp ? cx.edp[0][0] : evp[0];
                 evp[1] = dp ? cx.edp[0][1] : evp[1];
                 evp[2] = dp ? cx.edp[1][0] : evp[2];

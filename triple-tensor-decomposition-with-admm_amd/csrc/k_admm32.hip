@@ -56,8 +56,12 @@ __device__ __forceinline__ uint64_t ce32_word(float sv, int w) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(b, 2 * w + 1);
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ bool ce32_is_dense(float sv) {
-    return (ce32_word(sv, 0) & ce32_word(sv, 1) & ce32_word(sv, 2) & ce32_word(sv, 3)) == ~0ull;
+// a stored slot holds <= CE32_CAP < 64 nonzeros: mask word 0 is all ones only
+// for a dense tile (2 readlanes, not 8; k_admm.hip)
+__device__ __forceinline__ bool ce32_is_dense(float sv) { return ce32_word(sv, 0) == ~0ull; }
+__device__ __forceinline__ bool lane_bit32(uint64_t m, int lane) {
+    (void)lane;
+    return __builtin_amdgcn_inverse_ballot_w64(m);  // the uniform mask as the lane condition
 }
 // this lane's 4 elements from its slot word sv; true for a dense tile
 __device__ __forceinline__ bool ce32_decode(float sv, int lane, float (&e)[4]) {
@@ -70,10 +74,10 @@ __device__ __forceinline__ bool ce32_decode(float sv, int lane, float (&e)[4]) {
     for (int w = 0; w < 4; ++w) {
         const int src = (pre + lanes_below32(m[w])) & 63;
         const int v = __builtin_amdgcn_ds_bpermute(src << 2, b);
-        e[w] = ((m[w] >> lane) & 1) ? __int_as_float(v) : 0.0f;
+        e[w] = lane_bit32(m[w], lane) ? __int_as_float(v) : 0.0f;
         pre += __builtin_popcountll(m[w]);
     }
-    return (m[0] & m[1] & m[2] & m[3]) == ~0ull;
+    return m[0] == ~0ull;  // ce32_is_dense
 }
 // store this lane's 4 elements as the tile's slot (every lane one word), or
 // densely (wave-uniform, rare) when they do not fit.  cs: 128-float per-wave
@@ -95,7 +99,7 @@ __device__ __forceinline__ void ce32_encode(const float (&En)[4], int lane, floa
     int pre = 8;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        const int bit = dense ? 0 : (int)((nz[w] >> lane) & 1);
+        const int bit = (!dense && lane_bit32(nz[w], lane)) ? 1 : 0;
         const int at = pre + lanes_below32(nz[w]), away = 64 + lane;
         cs[away + ((at - away) & -bit)] = En[w];
         pre += __builtin_popcountll(nz[w]);
@@ -279,16 +283,21 @@ void k5_f32(K5Args32 a) {
                 const float L = Lv[r];
                 const float R1 = (d - L) + sc.invL * yl;               // :41
                 const float R2 = e - sc.invO * yo;                     // :42
-                const float On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
+                // x/den as reciprocal product + exact-residual FMA correction,
+                // sign()*max() as copysign (NaN kept): fewer VALU ops (k_admm.hip)
+                const float Onum = sc.muL * R1 + sc.muO * R2;
+                const float q0 = Onum * sc.rden;
+                const float On = fmaf(fmaf(-q0, sc.den, Onum), sc.rden, q0);  // :43
                 const float R3 = On + sc.invO * yo;                    // :46
-                const float Ev = sign32(R3) * fmaxf(fabsf(R3) - sc.thr, 0.0f);  // :47
+                float Ev = __builtin_copysignf(fmaxf(fabsf(R3) - sc.thr, 0.0f), R3);  // :47
+                Ev = (R3 != R3) ? R3 : Ev;
                 const float rL = (d - L) - On;                         // :50
                 const float rO = On - Ev;                              // :51
                 const float yln = yl + sc.muL * rL;                    // :52
                 const float yon = yo + sc.muO * rO;                    // :53
                 tr[r] = (d - On) + sc.invL_next * yln;                 // :33 (k+1)
-                ssL += (double)rL * (double)rL;
-                ssO += (double)rO * (double)rO;
+                ssL = fma((double)rL, (double)rL, ssL);
+                ssO = fma((double)rO, (double)rO, ssO);
                 En[r] = Ev;
                 YLn[r] = yln;
                 YOn[r] = yon;

@@ -176,6 +176,7 @@ void launch_quality(const double* X, const double* Y, int64_t n1, int64_t n2, in
 // ---------------------------------------------------------------------------
 struct IterScalars32 {
     float muL, muO, invL, invO, thr, den, invL_next;  // MATLAB: double scalar -> single
+    float rden;  // 1/den in single (K5's division, k_admm32.hip)
 };
 struct K5Args32 {
     const float* D;

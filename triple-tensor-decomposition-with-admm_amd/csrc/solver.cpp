@@ -323,6 +323,7 @@ IterScalars32 Session::scalars32(int k) const {
     s.invO = (float)d.invO;
     s.thr = (float)d.thr;
     s.den = (float)d.den;
+    s.rden = 1.0f / s.den;
     s.invL_next = (float)d.invL_next;
     return s;
 }
