@@ -5,7 +5,10 @@ Corrections (MI355X_MICROARCH.md §HBM): on gfx950 FETCH_SIZE reports half of
 the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE is
 exact for 16-B streaming stores.  Both counters are in KiB.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [algorithmic_bytes [kernel]]
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [algorithmic_bytes [kernel [first:last]]]
+(first:last: only dispatches first..last-1 in dispatch order, e.g. the bench's
+timed window; default all.  The config-5 solve densifies E after ~30
+iterations, so its later dispatches move more bytes than the timed window's.)
 (kernel: a substring of the kernel name, default "k5_fused<64, false", which matches
 the stored-Y_O and the derived-Y_O instantiations)
 """
@@ -25,9 +28,9 @@ def per_dispatch(d, counter, kname="k5_fused<64, false"):
                 continue
             if row.get("Counter_Name") != counter:
                 continue
-            key = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            key = int(row.get("Dispatch_Id") or row.get("Correlation_Id"))
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    return sorted(vals.values())
+    return [vals[k] for k in sorted(vals)]  # dispatch order
 
 
 def main():
@@ -36,12 +39,16 @@ def main():
     kname = sys.argv[5] if len(sys.argv) > 5 else "k5_fused<64, false"
     fetch = per_dispatch(fd, "FETCH_SIZE", kname)
     write = per_dispatch(wd, "WRITE_SIZE", kname)
+    window = None
+    if len(sys.argv) > 6:
+        a, b = (int(x) for x in sys.argv[6].split(":"))
+        fetch, write, window = fetch[a:b], write[a:b], [a, b]
     if not fetch or not write:
         raise SystemExit("no k5 dispatches found")
-    med = lambda v: v[len(v) // 2]
+    med = lambda v: sorted(v)[len(v) // 2]
     f_kib, w_kib = med(fetch), med(write)
     total = (2.0 * f_kib + w_kib) * 1024.0
-    res = {"kernel": kname, "dispatches": [len(fetch), len(write)],
+    res = {"kernel": kname, "dispatches": [len(fetch), len(write)], "window": window,
            "FETCH_SIZE_KiB_median": f_kib, "WRITE_SIZE_KiB_median": w_kib,
            "read_bytes_corrected": 2.0 * f_kib * 1024.0, "write_bytes": w_kib * 1024.0,
            "bytes_per_launch": total,

@@ -14,7 +14,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch
     python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- \
     python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/pmc_write.log 2>&1
-python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/${TAG}_k5_traffic.json $ALG
+python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/${TAG}_k5_traffic.json $ALG "k5_fused<64, false" 1:6  # the timed window (warmup 1, steps 5)
 cp $O/${TAG}_k5_traffic.json profiles/${TAG}_k5_traffic.json   # read by bench.py below
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
     python3 bench.py --no-cpu > $O/stats.log 2>&1
