@@ -214,7 +214,8 @@ def main():
     k5_ms = km["fused_update"]
     gbs = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
     tfs = k5_flops / (k5_ms * 1e-3) / 1e12 if k5_ms > 0 else None
-    traffic, traffic_src = pmc_traffic(args.config)
+    # the committed PMC pass is of the 1-GPU launch (a shard moves 1/N of it)
+    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
     if f32:  # config 5 is MFMA-bound
         roof = {"bound": "mfma", "achieved": tfs, "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": (tfs / F32_MFMA_PEAK_TFS) if tfs else None,
