@@ -43,6 +43,14 @@ CASES = {
     # r=8 exercises the R=64 (full MFMA tile) code path at a small size
     "g17x16x20_r8": (synth.low_rank_plus_outliers, dict(n1=17, n2=16, n3=20, r=8), 8,
                      dict(synth.TRAFFIC_OPTS, maxIter=25), False),
+    # fp64 r = 10, 12, 16: the padded-rank 128 / 256 kernels (K5 at one wave per
+    # SIMD, K2 in 64-column passes, generic apply, blocked / big solves)
+    "g20x18x16_r10": (synth.low_rank_plus_outliers, dict(n1=20, n2=18, n3=16, r=10), 10,
+                      dict(synth.TRAFFIC_OPTS, maxIter=20), False),
+    "g24x20x18_r12": (synth.low_rank_plus_outliers, dict(n1=24, n2=20, n3=18, r=12), 12,
+                      dict(synth.TRAFFIC_OPTS, maxIter=15), False),
+    "g24x22x20_r16": (synth.low_rank_plus_outliers, dict(n1=24, n2=22, n3=20, r=16), 16,
+                      dict(synth.TRAFFIC_OPTS, maxIter=10), False),
     # opts.model = 'qi' (SURVEY.md §8f rank 4): Qi-model builders of
     # origin_triple_tensor/, data drawn from the Qi triple product
     "qi12x10x8_r2": (synth.low_rank_plus_outliers, dict(n1=12, n2=10, n3=8, r=2, model="qi"), 2,
@@ -136,11 +144,13 @@ def make(name):
 
 
 if __name__ == "__main__":
-    # python tests/golden/make_golden.py [admm|qi|als|ncvx]  (default: all)
+    # python tests/golden/make_golden.py [admm|qi|wide|als|ncvx]  (default: all)
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
-    if which in ("all", "admm", "qi"):
+    if which in ("all", "admm", "qi", "wide"):
         for n in CASES:
             if which == "qi" and not n.startswith("qi"):
+                continue
+            if which == "wide" and n not in ("g20x18x16_r10", "g24x20x18_r12", "g24x22x20_r16"):
                 continue
             print(n, *make(n))
     if which in ("all", "als"):

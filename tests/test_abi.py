@@ -77,14 +77,19 @@ def test_python_api_raises_keyerror_for_missing_field():
                                  dict(mu=1, rho=1, **{"lambda": 1}, lambda2=1, maxIter=1, disp=0))
 
 
-def test_rank_above_fp64_kernels_is_unsupported(lib):
+def test_rank_above_the_kernels_is_unsupported(lib):
+    """ADMM: r <= 16 in either precision (fp64 r = 9..16 on the padded-rank
+    128/256 kernels); r = 17 is refused before any device work.  ALS keeps r <= 8."""
     D = np.zeros((4, 4, 4), order="F")
     o = _opts(lib)
-    big = np.zeros(4 * 81 * 4)
-    st = lib.lib.tritd_admm_f64(C.c_void_p(D.ctypes.data), 4, 4, 4, 9, C.byref(o),
+    big = np.zeros(4 * 17 * 17 * 4)
+    st = lib.lib.tritd_admm_f64(C.c_void_p(D.ctypes.data), 4, 4, 4, 17, C.byref(o),
                                 *[C.c_void_p(big.ctypes.data)] * 3, None, None, None, None, None,
                                 None, None, -1)
     assert st == 7  # TRITD_ERR_UNSUPPORTED
+    st = lib.lib.tritd_als_f64(C.c_void_p(D.ctypes.data), 4, 4, 4, 9, C.byref(o),
+                               *[C.c_void_p(big.ctypes.data)] * 3, None, None, None, None, None, -1)
+    assert st == 7
 
 
 def test_bad_unfold_mode_message(lib):

@@ -73,8 +73,9 @@ tritd_opts normalized(const tritd_opts* o) {
 void check_dims(int64_t n1, int64_t n2, int64_t n3, int32_t r, bool f32 = false) {
     if (n1 <= 0 || n2 <= 0 || n3 <= 0) throw Error(TRITD_ERR_ARG, "tensor dimensions must be positive");
     if (r <= 0) throw Error(TRITD_ERR_ARG, "rank r must be positive");
-    if (!f32 && r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "fp64 path supports r <= 8 (R = r^2 <= 64)");
-    if (f32 && r > 16) throw Error(TRITD_ERR_UNSUPPORTED, "fp32 path supports r <= 16 (R = r^2 <= 256)");
+    // wide = the ADMM paths (fp32 and fp64 r <= 16); ALS / test.m solver kernels stop at r = 8
+    if (!f32 && r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "this path supports r <= 8 (R = r^2 <= 64)");
+    if (f32 && r > 16) throw Error(TRITD_ERR_UNSUPPORTED, "r <= 16 (R = r^2 <= 256)");
 }
 
 void need(const void* p, const char* what) {
@@ -364,7 +365,7 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
     std::lock_guard<std::mutex> lk(g_mutex);
     return guarded([&] {
         check_opts(opts);
-        check_dims(n1, n2, n3, r);
+        check_dims(n1, n2, n3, r, true);  // fp64 ADMM: r <= 16 (r > 8 untuned)
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
         const tritd_opts o = normalized(opts);
         if (device < 0 && g_devices.size() > 1) {
@@ -582,7 +583,7 @@ tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t
     std::lock_guard<std::mutex> lk(g_mutex);
     return guarded([&] {
         check_opts(opts);
-        check_dims(n1, n2, n3, r);
+        check_dims(n1, n2, n3, r, true);  // fp64 ADMM: r <= 16 (r > 8 untuned)
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
         if (nshards < 1 || nshards > 16 || nshards > n1) throw Error(TRITD_ERR_ARG, "nshards must be in 1..min(16,n1)");
         const int dev = pick_device(device);

@@ -224,7 +224,7 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
 // Two waves per SIMD (VGPRs + AGPRs <= 256): at one wave per SIMD the
 // streams do not keep enough bytes in flight (measured +6 % K5 time).
 template <int RP, bool PRO, bool DY>
-__global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(RP >= 128 ? 1 : 2, 2)))
 void k5_fused(K5Args a) {
     if (*a.stop) return;
     constexpr int KS = RP / 4;   // MFMA K-steps for L
@@ -648,6 +648,8 @@ void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream
         K5_CASE(32)
         K5_CASE(48)
         K5_CASE(64)
+        K5_CASE(128)  // r = 9..16 (fp64): one wave per SIMD, 146 KB of LDS at 256
+        K5_CASE(256)
         default:
             throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by K5");
     }

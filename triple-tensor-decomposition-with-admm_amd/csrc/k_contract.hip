@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
                                                const double* __restrict__ Bh, double* part,
                                                int64_t n1p, int64_t n3p, int64_t ntt,
                                                int64_t tiles, int S, const int* stop,
-                                               int64_t ahj, int64_t bhj) {
+                                               int64_t ahj, int64_t bhj, int lda) {
     if (*stop) return;
     constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
             const double bh = Bh[j * bhj + k];
             double a[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) a[s] = Aj[(i0 + 4 * s + tg) * RP + k] * bh;
+            for (int s = 0; s < 4; ++s) a[s] = Aj[(i0 + 4 * s + tg) * lda + k] * bh;
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
     }
     __syncthreads();
     if (wid == 0) {
-        double* out = part + (int64_t)(sidx >> 2) * n3p * RP;
+        double* out = part + (int64_t)(sidx >> 2) * n3p * lda;  // slabs of n3p x lda
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
                     const double v = acc[m][n][rr] + lds[((m * 4 + n) * 4 + rr) * 64 + lane];
                     const int64_t t = tb * 64 + 16 * n + il;
                     const int k = 16 * m + tg + 4 * rr;
-                    if (t < n3p) out[t * RP + k] = v;
+                    if (t < n3p) out[t * lda + k] = v;
                 }
     }
 }
@@ -272,8 +272,11 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
     const int S = m3_split(g);
     const int64_t ntb = cdiv(g.ntt, 4);
     const dim3 grid((unsigned)(ntb * S / 4));
-#define M3_CASE(RPV)                                                                          \
-    case RPV: {                                                                               \
+    // RP <= 64 in one pass; RP = 128 / 256 (fp64 r = 9..16) as 64-column
+    // passes over the same T (their columns of the factor rows and of the
+    // partial slabs, whose row stride stays RP)
+#define M3_CASE(RPV, KOFF)                                                                    \
+    {                                                                                         \
         const size_t lds = (size_t)2 * (RPV / 16) * 16 * 64 * sizeof(double);                \
         static bool attr_set = false;                                                         \
         if (!attr_set) {                                                                      \
@@ -281,14 +284,18 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
             attr_set = true;                                                                  \
         }                                                                                     \
-        hipLaunchKernelGGL(k_m3<RPV>, grid, dim3(256), lds, st, T, Ah, Bh, part, g.n1p, g.n3p, \
-                           g.ntt, g.tiles, S, stop, ahj, bhj);                                \
-    } break;
+        hipLaunchKernelGGL(k_m3<RPV>, grid, dim3(256), lds, st, T, Ah + (KOFF), Bh + (KOFF),   \
+                           part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj, g.RP); \
+    }
     switch (g.RP) {
-        M3_CASE(16)
-        M3_CASE(32)
-        M3_CASE(48)
-        M3_CASE(64)
+        case 16: M3_CASE(16, 0) break;
+        case 32: M3_CASE(32, 0) break;
+        case 48: M3_CASE(48, 0) break;
+        case 64: M3_CASE(64, 0) break;
+        case 128:
+        case 256:
+            for (int k0 = 0; k0 < g.RP; k0 += 64) M3_CASE(64, k0)
+            break;
         default:
             throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by M3");
     }

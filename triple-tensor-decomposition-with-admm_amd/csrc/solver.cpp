@@ -79,7 +79,10 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     g_ = make_geom(n1, n2, n3, i0, i1, r);
     f32_ = (flags & TRITD_SESSION_F32) != 0;
     es_ = f32_ ? sizeof(float) : sizeof(double);
-    if (f32_) g_.RP = padded_rank32(g_.R);
+    // fp32 path and fp64 r = 9..16: padded ranks 16/32/48/64/128/256 (the
+    // K5 / K2 instantiations; fp64 RP = 128/256 runs K5 at one wave per SIMD
+    // and K2 as 64-column passes — functional, not the tuned r <= 8 path)
+    if (f32_ || g_.R > 64) g_.RP = padded_rank32(g_.R);
     overlap_ = (comm == nullptr) && (shared_stream == nullptr);
     {
         const char* ov = std::getenv("TRITD_OVERLAP");
@@ -109,9 +112,9 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         throw Error(TRITD_ERR_ARG, "opts.model must be 'cp' or 'qi'");
     if (qi_ && f32_)
         throw Error(TRITD_ERR_UNSUPPORTED, "opts.model='qi' is implemented for a double D only");
-    if (f32_ ? !rp_supported32(g_.RP) : !rp_supported(g_.RP))
-        throw Error(TRITD_ERR_UNSUPPORTED,
-                    f32_ ? "r must be in 1..16 for the fp32 path" : "r must be in 1..8 for the fp64 path");
+    if (!rp_supported32(g_.RP))
+        throw Error(TRITD_ERR_UNSUPPORTED, "r must be in 1..16");
+    if (qi_ && g_.r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "opts.model='qi': r <= 8");
 
     // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
     mu_.resize((size_t)o_.maxIter + 2);
@@ -378,6 +381,9 @@ void Session::do_apply_A(const double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, nullptr, M1_.f(), g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
                          true, ctrl_, st_);
+    else if (g_.RP > 64)  // fp64 r = 9..16
+        launch_apply_gen(g_.RP, M1_.p, nullptr, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
+                         false, ctrl_, st_);
     else
         launch_apply(g_.RP, M1_.p, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
 }
@@ -385,6 +391,9 @@ void Session::do_apply_A(const double* Ginv) {
 void Session::do_apply_B(const double* M2, const double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, true, ctrl_,
+                         st_);
+    else if (g_.RP > 64)  // fp64 r = 9..16
+        launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, false, ctrl_,
                          st_);
     else
         launch_apply(g_.RP, M2, g_.n2, Ginv, Bh_.p, nullptr, 0, ctrl_, st_);
@@ -394,6 +403,9 @@ void Session::do_apply_C(const double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ChF_.f(),
                          true, ctrl_, st_);
+    else if (g_.RP > 64)  // fp64 r = 9..16
+        launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, nullptr,
+                         false, ctrl_, st_);
     else
         launch_apply(g_.RP, red2_.p, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
 }
