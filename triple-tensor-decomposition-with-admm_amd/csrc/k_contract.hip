@@ -126,13 +126,14 @@ void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, c
 // ---------------------------------------------------------------------------
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-template <int RP>
+template <int RP, int LDA>  // LDA: row stride of the factor rows and the slabs (RP, or 128/256 in 64-column passes)
 __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
                                                const double* __restrict__ Ah,
                                                const double* __restrict__ Bh, double* part,
                                                int64_t n1p, int64_t n3p, int64_t ntt,
                                                int64_t tiles, int S, const int* stop,
-                                               int64_t ahj, int64_t bhj, int lda) {
+                                               int64_t ahj, int64_t bhj) {
+    constexpr int lda = LDA;
     if (*stop) return;
     constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -275,26 +276,28 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
     // RP <= 64 in one pass; RP = 128 / 256 (fp64 r = 9..16) as 64-column
     // passes over the same T (their columns of the factor rows and of the
     // partial slabs, whose row stride stays RP)
-#define M3_CASE(RPV, KOFF)                                                                    \
+#define M3_CASE(RPV, LDAV, KOFF)                                                              \
     {                                                                                         \
         const size_t lds = (size_t)2 * (RPV / 16) * 16 * 64 * sizeof(double);                \
         static bool attr_set = false;                                                         \
         if (!attr_set) {                                                                      \
-            TRITD_HIP(hipFuncSetAttribute((const void*)k_m3<RPV>,                             \
+            TRITD_HIP(hipFuncSetAttribute((const void*)k_m3<RPV, LDAV>,                       \
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
             attr_set = true;                                                                  \
         }                                                                                     \
-        hipLaunchKernelGGL(k_m3<RPV>, grid, dim3(256), lds, st, T, Ah + (KOFF), Bh + (KOFF),   \
-                           part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj, g.RP); \
+        hipLaunchKernelGGL((k_m3<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF),       \
+                           Bh + (KOFF), part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj); \
     }
     switch (g.RP) {
-        case 16: M3_CASE(16, 0) break;
-        case 32: M3_CASE(32, 0) break;
-        case 48: M3_CASE(48, 0) break;
-        case 64: M3_CASE(64, 0) break;
+        case 16: M3_CASE(16, 16, 0) break;
+        case 32: M3_CASE(32, 32, 0) break;
+        case 48: M3_CASE(48, 48, 0) break;
+        case 64: M3_CASE(64, 64, 0) break;
         case 128:
+            for (int k0 = 0; k0 < 128; k0 += 64) M3_CASE(64, 128, k0)
+            break;
         case 256:
-            for (int k0 = 0; k0 < g.RP; k0 += 64) M3_CASE(64, k0)
+            for (int k0 = 0; k0 < 256; k0 += 64) M3_CASE(64, 256, k0)
             break;
         default:
             throw Error(TRITD_ERR_UNSUPPORTED, "rank not supported by M3");
