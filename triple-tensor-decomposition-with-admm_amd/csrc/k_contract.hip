@@ -19,6 +19,7 @@
 namespace tritd {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -73,7 +74,7 @@ void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, co
     // 4 slices when the row blocks alone fill the chip (512 rows: 36 vs 39 us
     // with 16), 16 for short shards (64 rows: 64 blocks)
     const dim3 grid((unsigned)cdiv(g.n1p, 64), g.RP);
-    if (g.n1p >= 256)
+    if (g.n1p >= 256)  // (two rows per lane with 16-B loads halves the waves: 72 vs 36 us)
         hipLaunchKernelGGL(k_m1<4>, grid, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
                            g.RP, stop);
     else
@@ -94,10 +95,16 @@ __global__ __launch_bounds__(256) void k_m2(const double* __restrict__ Wk,
     const int64_t j = blockIdx.x;
     const int k = blockIdx.y * 4 + w;
     if (k >= RP) return;
-    const double* wp = Wk + (int64_t)k * plane + j * n1p;
-    const double* ap = AhT + (int64_t)k * n1p;
-    double acc = 0.0;
-    for (int64_t i = lane; i < n1p; i += 64) acc = fma(wp[i], ap[i], acc);
+    // 16-B loads (n1p % 16 == 0): lane sums rows 2l, 2l+1, 2l+128, ... in two chains
+    const d2v* wp = reinterpret_cast<const d2v*>(Wk + (int64_t)k * plane + j * n1p);
+    const d2v* ap = reinterpret_cast<const d2v*>(AhT + (int64_t)k * n1p);
+    double a0 = 0.0, a1 = 0.0;
+    for (int64_t q = lane; q < (n1p >> 1); q += 64) {
+        const d2v x = wp[q], y = ap[q];
+        a0 = fma(x.x, y.x, a0);
+        a1 = fma(x.y, y.y, a1);
+    }
+    double acc = a0 + a1;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
     if (lane == 0) M2[j * RP + k] = acc;
@@ -124,7 +131,6 @@ void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, c
 // workgroup share the t-block and are summed through LDS in fixed order;
 // the per-workgroup partials are summed by k_m3_reduce in fixed order.
 // ---------------------------------------------------------------------------
-typedef double d2v __attribute__((ext_vector_type(2)));
 
 template <int RP, int LDA>  // LDA: row stride of the factor rows and the slabs (RP, or 128/256 in 64-column passes)
 __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
