@@ -141,6 +141,29 @@ def test_medium_against_oracle(tritd, orc):
     np.testing.assert_allclose(eh, ref[4], rtol=TOL_ERR, atol=ATOL_ERR)
 
 
+@pytest.mark.parametrize("shape,r", [((12, 10), 2), ((5, 1, 7), 2), ((1, 9, 8), 2), ((33, 17, 1), 3),
+                                     ((16, 16, 16), 1)])
+def test_degenerate_shapes_against_oracle(tritd, orc, shape, r):
+    """2-D D (n3 = 1 by MATLAB's trailing-singleton rule), singleton modes and r = 1:
+    ragged single tiles in every padded dimension."""
+    rng = np.random.default_rng(11)
+    D = np.asfortranarray(rng.standard_normal(shape) * 3.0)
+    n1, n2, n3 = (tuple(shape) + (1,))[:3]
+    A0 = rng.standard_normal((n1, r, r))
+    B0 = rng.standard_normal((r, n2, r))
+    C0 = rng.standard_normal((r, r, n3))
+    from tritd import synth
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=8)
+    ref = orc.triple_decomp_ADMM(D, r, opts, A0, B0, C0)
+    A, B, C, O, eh, E, k = tritd.triple_decomp_ADMM(D, r, opts, A0, B0, C0, return_E=True,
+                                                    return_iters=True)
+    assert k == ref[6]
+    assert rel(orc.triple_product(A, B, C), orc.triple_product(ref[0], ref[1], ref[2])) <= 1e-8
+    assert rel(O, ref[3]) <= 1e-8
+    assert rel(E, ref[5]) <= 1e-8
+    np.testing.assert_allclose(eh, ref[4], rtol=1e-7, atol=1e-11)
+
+
 def test_disp_prints_like_reference(tritd, orc):
     g = load_golden("g30_r3")
     opts = dict(g["opts"], disp=1, maxIter=20)
