@@ -148,21 +148,28 @@ static constexpr int QW = 11;            // window edge
 static constexpr int QI = QT + QW - 1;   // input tile edge (26)
 
 // SSIM map tiles: block (tx, ty, frame) computes a QT x QT tile of the
-// (n1-10) x (n2-10) 'valid' map directly in 2-D (filter2 is a correlation;
-// the Gaussian window is symmetric), and its partial sum of the map.
+// (n1-10) x (n2-10) 'valid' map and its partial sum (filter2 is a
+// correlation; the Gaussian window is symmetric).  The window of
+// ssim_index.m is fspecial('gaussian',11,1.5) normalised, i.e. g g' up to
+// rounding (no entry reaches fspecial's eps cut-off), so the five local
+// moments are filtered separably: g(u) = win(u,c)/sqrt(win(c,c)), c = 5,
+// first along j (26 x 16 partials in LDS), then along i -- 22 taps per
+// moment instead of 121.  Rounding differs from the 2-D sum by a few ulps.
 __global__ __launch_bounds__(QT* QT) void k_ssim_tiles(const double* __restrict__ X,
                                                        const double* __restrict__ Y, int64_t n1,
                                                        int64_t n2, const double* __restrict__ win,
                                                        double C1, double C2,
                                                        double* __restrict__ part) {
-    __shared__ double sx[QI][QI + 1], sy[QI][QI + 1];
-    __shared__ double w[QW * QW];
+    __shared__ double sx[QI][QI + 1], sy[QI][QI + 1];   // [column offset][row offset]
+    __shared__ double hm[5][QT][QI + 1];                // j-filtered moments [out column][row]
+    __shared__ double g[QW];
     const int tx = threadIdx.x % QT, ty = threadIdx.x / QT;  // tx along rows i (fast)
     const int64_t f = blockIdx.z;
     const int64_t i0 = (int64_t)blockIdx.x * QT, j0 = (int64_t)blockIdx.y * QT;
     const double* Xf = X + f * n1 * n2;
     const double* Yf = Y + f * n1 * n2;
-    if (threadIdx.x < QW * QW) w[threadIdx.x] = win[threadIdx.x];
+    constexpr int c = QW / 2;
+    if (threadIdx.x < QW) g[threadIdx.x] = win[c * QW + threadIdx.x] / sqrt(win[c * QW + c]);
     for (int e = threadIdx.x; e < QI * QI; e += QT * QT) {
         const int a = e % QI, b = e / QI;  // a: row offset, b: column offset
         const int64_t i = i0 + a, j = j0 + b;
@@ -171,24 +178,40 @@ __global__ __launch_bounds__(QT* QT) void k_ssim_tiles(const double* __restrict_
         sy[b][a] = in ? Yf[j * n1 + i] : 0.0;
     }
     __syncthreads();
+    for (int e = threadIdx.x; e < QT * QI; e += QT * QT) {
+        const int a = e % QI, b = e / QI;  // row a of the input tile, output column b
+        double m1 = 0.0, m2 = 0.0, s11 = 0.0, s22 = 0.0, s12 = 0.0;
+#pragma unroll
+        for (int v2 = 0; v2 < QW; ++v2) {
+            const double wt = g[v2];
+            const double x = sx[b + v2][a], y = sy[b + v2][a];
+            m1 += wt * x;
+            m2 += wt * y;
+            s11 += wt * (x * x);
+            s22 += wt * (y * y);
+            s12 += wt * (x * y);
+        }
+        hm[0][b][a] = m1;
+        hm[1][b][a] = m2;
+        hm[2][b][a] = s11;
+        hm[3][b][a] = s22;
+        hm[4][b][a] = s12;
+    }
+    __syncthreads();
     const int64_t mi = n1 - (QW - 1), mj = n2 - (QW - 1);  // valid map size
     const int64_t oi = i0 + tx, oj = j0 + ty;
     double v = 0.0;
     if (oi < mi && oj < mj) {
-        double m1 = 0.0, m2 = 0.0, s11 = 0.0, s22 = 0.0, s12 = 0.0;
-        for (int v2 = 0; v2 < QW; ++v2) {      // window column (j offset)
-            for (int u = 0; u < QW; ++u) {     // window row (i offset)
-                const double wt = w[v2 * QW + u];  // win(u, v2), column-major
-                const double a = sx[ty + v2][tx + u], b = sy[ty + v2][tx + u];
-                m1 += wt * a;
-                m2 += wt * b;
-                s11 += wt * (a * a);
-                s22 += wt * (b * b);
-                s12 += wt * (a * b);
-            }
+        double m[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+            const double wt = g[u];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) m[q] += wt * hm[q][ty][tx + u];
         }
+        const double m1 = m[0], m2 = m[1];
         const double mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu1_mu2 = m1 * m2;
-        const double sigma1_sq = s11 - mu1_sq, sigma2_sq = s22 - mu2_sq, sigma12 = s12 - mu1_mu2;
+        const double sigma1_sq = m[2] - mu1_sq, sigma2_sq = m[3] - mu2_sq, sigma12 = m[4] - mu1_mu2;
         v = ((2 * mu1_mu2 + C1) * (2 * sigma12 + C2)) /
             ((mu1_sq + mu2_sq + C1) * (sigma1_sq + sigma2_sq + C2));
     }
