@@ -60,7 +60,7 @@ static constexpr int K5_WAVES = 4;
 #define K5_SMASK 0
 #endif
 #ifndef K5_CSIGN
-#define K5_CSIGN 1
+#define K5_CSIGN 2
 #endif
 #ifndef K5_IBAL
 #define K5_IBAL 1
@@ -500,7 +500,13 @@ void k5_fused(K5Args a) {
                     const double On = (sc.muL * R1 + sc.muO * R2) / sc.den; // :43
 #endif
                     const double R3 = On + sc.invO * yo;                    // :46
-#if K5_CSIGN
+#if K5_CSIGN == 2
+                    // sign(R3).*max(abs(R3)-thr,0) as R3 - clamp(R3,-thr,thr)
+                    // (thr >= 0): |R3| > thr gives R3 -/+ thr, the same rounded
+                    // difference; otherwise a zero (possibly -0 where MATLAB has
+                    // +0); NaN and Inf pass through.  3 VALU ops instead of 10
+                    const double Ev = R3 - fmin(fmax(R3, -sc.thr), sc.thr);  // :47
+#elif K5_CSIGN
                     // sign(R3).*max(abs(R3)-thr,0) as copysign (thr > 0): equal
                     // values (a zero may come out as -0), NaN kept; 7 VALU ops
                     // instead of 10

@@ -284,13 +284,12 @@ void k5_f32(K5Args32 a) {
                 const float R1 = (d - L) + sc.invL * yl;               // :41
                 const float R2 = e - sc.invO * yo;                     // :42
                 // x/den as reciprocal product + exact-residual FMA correction,
-                // sign()*max() as copysign (NaN kept): fewer VALU ops (k_admm.hip)
+                // sign()*max() as R3 - clamp(R3,-thr,thr): fewer VALU ops (k_admm.hip)
                 const float Onum = sc.muL * R1 + sc.muO * R2;
                 const float q0 = Onum * sc.rden;
                 const float On = fmaf(fmaf(-q0, sc.den, Onum), sc.rden, q0);  // :43
                 const float R3 = On + sc.invO * yo;                    // :46
-                float Ev = __builtin_copysignf(fmaxf(fabsf(R3) - sc.thr, 0.0f), R3);  // :47
-                Ev = (R3 != R3) ? R3 : Ev;
+                const float Ev = R3 - fminf(fmaxf(R3, -sc.thr), sc.thr);  // :47
                 const float rL = (d - L) - On;                         // :50
                 const float rO = On - Ev;                              // :51
                 const float yln = yl + sc.muL * rL;                    // :52
