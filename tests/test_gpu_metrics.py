@@ -49,6 +49,54 @@ def test_evaluate_size_mismatch_and_empty(tritd):
     assert r == 1.0 and n == pytest.approx(1.0 / np.sqrt(5.0), rel=1e-15)
 
 
+def test_evaluate_more_true_entries_than_gt(tritd):
+    """nnz(mask) > numel(gt): MATLAB's size error; the kernels read gt only below m."""
+    mask = np.zeros((33, 40, 9), dtype=bool)
+    mask.ravel()[::7] = True
+    with pytest.raises(tritd.TritdError, match="incompatible sizes"):
+        tritd.evaluate(np.ones(mask.shape), np.ones(5), mask)
+
+
+@pytest.mark.parametrize("n,offset", [(1 << 20, 1), (100003, 3), (4097, 0), (15, 1)])
+def test_evaluate_device_mask_unaligned_and_ragged(tritd, orc, n, offset):
+    """tritd_dev_evaluate_f64 on device buffers: a mask pointer off the 16-byte
+    grid (byte-load path) and lengths that end inside a 16-position group or a
+    wave chunk."""
+    import ctypes as C
+    from tritd import _lib
+    hip = C.CDLL("libamdhip64.so")  # the runtime libtritd.so already loaded
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipFree.argtypes = [C.c_void_p]
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal(n)
+    mk = np.zeros(n + 16, dtype=np.uint8)
+    mk[offset:offset + n] = rng.random(n) < 0.3
+    gt = rng.standard_normal(int(mk.sum()))
+    bufs = []
+
+    def dev(a):
+        p = C.c_void_p()
+        assert hip.hipMalloc(C.byref(p), C.c_size_t(max(a.nbytes, 1))) == 0
+        bufs.append(p)
+        assert hip.hipMemcpy(p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes), 1) == 0  # H2D
+        return p.value
+
+    try:
+        Xd, gd, mb = dev(X), dev(gt), dev(mk)
+        rm, nr = C.c_double(0), C.c_double(0)
+        st = _lib.lib.tritd_dev_evaluate_f64(C.c_void_p(Xd), n, C.c_void_p(gd), gt.size,
+                                              C.c_void_p(mb + offset), C.byref(rm), C.byref(nr), None)
+        assert hip.hipDeviceSynchronize() == 0
+    finally:
+        for p in bufs:
+            hip.hipFree(p)
+    assert st == 0
+    mk = mk[offset:offset + n].astype(bool)
+    r_ref, n_ref = orc.evaluate(X[mk], gt)
+    assert rm.value == pytest.approx(r_ref, rel=1e-12) and nr.value == pytest.approx(n_ref, rel=1e-12)
+
+
 @pytest.mark.parametrize("shape", [(40, 50, 4), (240, 320, 6), (11, 11, 2), (64, 17, 3)])
 def test_quality_matches_oracle(tritd, orc, shape):
     rng = np.random.default_rng(6)

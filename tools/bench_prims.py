@@ -88,8 +88,8 @@ def main():
     gt = torch.randn(m, dtype=torch.float64, device=dev, generator=g)
     ms = timed(lambda: check(lib.tritd_dev_evaluate_f64(p(X), N, p(gt), m, p(mask), C.byref(rm),
                                                        C.byref(nr), sp)), a.reps, st)
-    # mask read twice (count + pairing), X at the true positions (whole 64 B
-    # sectors at 10 % density), gt once
+    # mask read twice (count + pairing), X at the true positions (counted as
+    # all of X: at 10 % density most 64 B sectors hold one), gt once
     rec("evaluate_masked10", ms, 2 * N + N * 8 + m * 8)
 
     n1, n2, nf = 240, 320, 300  # the Highway video shape (config 3)

@@ -938,15 +938,14 @@ tritd_status tritd_dev_evaluate_f64(const double* X, int64_t n, const double* gt
             int64_t* sc = nullptr;
             TRITD_HIP(hipMalloc(&sc, (size_t)(nb + 1) * sizeof(int64_t)));
             struct Free { int64_t* p; ~Free() { (void)hipFree(p); } } fr{sc};
-            launch_evaluate(X, gt, mask, n, sc, part.p, out.p, sc + nb, st);
+            launch_evaluate(X, gt, m, mask, n, sc, part.p, out.p, sc + nb, st);
             int64_t total = n;
             if (mask)
                 TRITD_HIP(hipMemcpyAsync(&total, sc + nb, sizeof total, hipMemcpyDeviceToHost, st));
             TRITD_HIP(hipMemcpyAsync(h, out.p, sizeof h, hipMemcpyDeviceToHost, st));
             TRITD_HIP(hipStreamSynchronize(st));
             // X(mask)-gt(:) with numel(X(mask)) ~= numel(gt) fails in MATLAB
-            // (gt was read only up to m entries: positions past it are not touched
-            // because the check below precedes any use of the sums)
+            // (the kernels read gt only below m; the sums are unused then)
             if (total != m) throw Error(TRITD_ERR_ARG, "Arrays have incompatible sizes for this operation.");
         } else if (m != 0) {
             throw Error(TRITD_ERR_ARG, "Arrays have incompatible sizes for this operation.");

@@ -11,7 +11,7 @@
 //                              filter2 'valid', mean2 of the map)
 // Both are HBM-bound streaming reductions with fixed-order (deterministic)
 // partial sums; the masked evaluate pairs the k-th true mask position (column-
-// major order, MATLAB's X(mask)) with gt(k) through a block-count scan.
+// major order, MATLAB's X(mask)) with gt(k) through a wave-count scan.
 #include "kernels.h"
 
 namespace tritd {
@@ -32,18 +32,58 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
     return s;
 }
 
-// pass 1: number of true mask entries per chunk
-__global__ __launch_bounds__(EV_THREADS) void k_mask_count(const uint8_t* __restrict__ mask,
-                                                           int64_t n, int64_t* __restrict__ cnt) {
-    const int64_t base = (int64_t)blockIdx.x * EV_CHUNK;
-    int c = 0;
-    for (int q = 0; q < EV_ROUNDS; ++q) {
-        const int64_t e = base + (int64_t)q * EV_THREADS + threadIdx.x;
-        c += (e < n && mask[e]) ? 1 : 0;
+// Masked pass layout: wave w owns the EV_CHUNK = 4096 consecutive positions
+// [4096 w, 4096 w + 4096) as 4 rounds in which lane l holds the 16 positions
+// 1024 q + 16 l + (0..15) (one 16-byte mask load).  A position's rank among
+// the true ones is the wave's offset + the true positions of lower lanes
+// (the lane counts' bits, ballot by ballot) + those before it in its group.
+static constexpr int MG = 16;                    // positions per lane per round
+static constexpr int MROUNDS = (int)(EV_CHUNK / (64 * MG));
+static_assert(MROUNDS * 64 * MG == EV_CHUNK, "wave chunk");
+
+// bit b set <=> mask[e + b] != 0, b < 16 (positions past n read as false)
+__device__ __forceinline__ uint32_t mask_bits(const uint8_t* __restrict__ mask, int64_t e, int64_t n,
+                                              bool al) {
+    uint32_t bits = 0;
+    if (al && e + MG <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(mask + e);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < MG; ++k) bits |= (((w[k >> 2] >> (8 * (k & 3))) & 0xffu) != 0u) << k;
+    } else {
+        for (int k = 0; k < MG; ++k)
+            if (e + k < n && mask[e + k]) bits |= 1u << k;
     }
-    __shared__ double sh[EV_THREADS / 64];
-    const double s = block_sum((double)c, sh);
-    if (threadIdx.x == 0) cnt[blockIdx.x] = (int64_t)s;
+    return bits;
+}
+
+// exclusive prefix over the lanes of c (0 <= c <= 16) and the wave total
+__device__ __forceinline__ void wave_scan16(int c, int& below, int& total) {
+    below = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint64_t bal = __ballot((c >> k) & 1);
+        below += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u)) << k;
+        total += __builtin_popcountll(bal) << k;
+    }
+}
+
+// pass 1: number of true mask entries per wave chunk
+__global__ __launch_bounds__(EV_THREADS) void k_mask_count(const uint8_t* __restrict__ mask,
+                                                           int64_t n, int nw, int al,
+                                                           int64_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)blockIdx.x * (EV_THREADS / 64) + (int)(threadIdx.x >> 6);
+    if (gw >= nw) return;
+    const int64_t base = (int64_t)gw * EV_CHUNK;
+    int c = 0;
+    for (int q = 0; q < MROUNDS; ++q)
+        c += __builtin_popcount(mask_bits(mask, base + q * 64 * MG + MG * lane, n, al != 0));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) cnt[gw] = c;
 }
 
 // pass 2: exclusive scan of the chunk counts (one block, sequential carry)
@@ -69,41 +109,59 @@ __global__ __launch_bounds__(EV_THREADS) void k_scan_counts(int64_t* __restrict_
     if (threadIdx.x == 0) *total = carry;
 }
 
-// pass 3: sum (X(p) - gt(k))^2 and gt(k)^2 over the true positions p (k-th
-// true position <-> gt(k)); mask == null pairs X(p) with gt(p).
-__global__ __launch_bounds__(EV_THREADS) void k_eval_masked(const double* __restrict__ X,
-                                                            const double* __restrict__ gt,
-                                                            const uint8_t* __restrict__ mask,
-                                                            const int64_t* __restrict__ off,
-                                                            int64_t n, double* __restrict__ part) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// pass 3 (mask): sum (X(p) - gt(k))^2 and gt(k)^2 over the true positions p,
+// k = rank of p among them; only X at true positions is loaded
+__global__ __launch_bounds__(EV_THREADS) void k_eval_mask(const double* __restrict__ X,
+                                                          const double* __restrict__ gt, int64_t m,
+                                                          const uint8_t* __restrict__ mask,
+                                                          const int64_t* __restrict__ off,
+                                                          int64_t n, int nw, int al,
+                                                          double* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)blockIdx.x * (EV_THREADS / 64) + (int)(threadIdx.x >> 6);
+    double sd = 0.0, sg = 0.0;
+    if (gw < nw) {
+        const int64_t base = (int64_t)gw * EV_CHUNK;
+        int64_t k0 = off[gw];
+        for (int q = 0; q < MROUNDS; ++q) {
+            const int64_t e = base + q * 64 * MG + MG * lane;
+            const uint32_t bits = mask_bits(mask, e, n, al != 0);
+            int below, tot;
+            wave_scan16(__builtin_popcount(bits), below, tot);
+            int64_t k = k0 + below;
+#pragma unroll
+            for (int b = 0; b < MG; ++b) {
+                if ((bits >> b) & 1u) {
+                    if (k < m) {
+                        const double g = gt[k];
+                        const double d = X[e + b] - g;
+                        sd += d * d;
+                        sg += g * g;
+                    }
+                    ++k;
+                }
+            }
+            k0 += tot;
+        }
+    }
+    __shared__ double sh[EV_THREADS / 64];
+    const double a = block_sum(sd, sh);
+    const double b = block_sum(sg, sh);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = b;
+    }
+}
+
+// pass 3 (no mask): X and gt paired elementwise
+__global__ __launch_bounds__(EV_THREADS) void k_eval_full(const double* __restrict__ X,
+                                                          const double* __restrict__ gt,
+                                                          int64_t n, double* __restrict__ part) {
     const int64_t base = (int64_t)blockIdx.x * EV_CHUNK;
-    __shared__ int wcnt[EV_THREADS / 64];
-    int64_t k0 = mask ? off[blockIdx.x] : 0;
     double sd = 0.0, sg = 0.0;
     for (int q = 0; q < EV_ROUNDS; ++q) {
         const int64_t e = base + (int64_t)q * EV_THREADS + threadIdx.x;
-        const bool in = e < n;
-        if (mask) {
-            const bool m = in && mask[e];
-            const uint64_t bal = __ballot(m);
-            const int below = (int)__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            if (lane == 0) wcnt[wid] = __builtin_popcountll(bal);
-            __syncthreads();
-            int pre = 0;
-            for (int w = 0; w < wid; ++w) pre += wcnt[w];
-            int tot = 0;
-            for (int w = 0; w < EV_THREADS / 64; ++w) tot += wcnt[w];
-            if (m) {
-                const double g = gt[k0 + pre + below];
-                const double d = X[e] - g;
-                sd += d * d;
-                sg += g * g;
-            }
-            k0 += tot;
-            __syncthreads();
-        } else if (in) {
+        if (e < n) {
             const double g = gt[e];
             const double d = X[e] - g;
             sd += d * d;
@@ -121,23 +179,29 @@ __global__ __launch_bounds__(EV_THREADS) void k_eval_masked(const double* __rest
 
 int64_t evaluate_blocks(int64_t n) { return cdiv(n, EV_CHUNK); }
 
-void launch_evaluate(const double* X, const double* gt, const uint8_t* mask, int64_t n,
+void launch_evaluate(const double* X, const double* gt, int64_t m, const uint8_t* mask, int64_t n,
                      int64_t* scratch_i64, double* part, double* out2, int64_t* total,
                      hipStream_t st) {
     const int64_t nb = evaluate_blocks(n);
-    if (nb > (int64_t)INT32_MAX) throw Error(TRITD_ERR_ARG, "tensor too large for evaluate");
+    if (nb > (int64_t)INT32_MAX / 4) throw Error(TRITD_ERR_ARG, "tensor too large for evaluate");
     if (mask) {
-        hipLaunchKernelGGL(k_mask_count, dim3((unsigned)nb), dim3(EV_THREADS), 0, st, mask, n,
+        const int nw = (int)nb;  // one wave per EV_CHUNK positions
+        const unsigned grid = (unsigned)cdiv(nb, EV_THREADS / 64);
+        const int al = ((uintptr_t)mask & 15) == 0;
+        hipLaunchKernelGGL(k_mask_count, dim3(grid), dim3(EV_THREADS), 0, st, mask, n, nw, al,
                            scratch_i64);
         TRITD_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(EV_THREADS), 0, st, scratch_i64, (int)nb,
-                           total);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(EV_THREADS), 0, st, scratch_i64, nw, total);
         TRITD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_eval_mask, dim3(grid), dim3(EV_THREADS), 0, st, X, gt, m, mask,
+                           scratch_i64, n, nw, al, part);
+        TRITD_CHECK_LAUNCH();
+        launch_reduce_pairs(part, (int)grid, out2, nullptr, st);
+    } else {
+        hipLaunchKernelGGL(k_eval_full, dim3((unsigned)nb), dim3(EV_THREADS), 0, st, X, gt, n, part);
+        TRITD_CHECK_LAUNCH();
+        launch_reduce_pairs(part, (int)nb, out2, nullptr, st);
     }
-    hipLaunchKernelGGL(k_eval_masked, dim3((unsigned)nb), dim3(EV_THREADS), 0, st, X, gt, mask,
-                       scratch_i64, n, part);
-    TRITD_CHECK_LAUNCH();
-    launch_reduce_pairs(part, (int)nb, out2, nullptr, st);
 }
 
 // ---------------------------------------------------------------------------

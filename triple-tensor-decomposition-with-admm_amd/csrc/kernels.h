@@ -155,11 +155,13 @@ void launch_ncvx_shrink(const Geom& g, double* Ah, double* AhT, double gamma, do
 
 // ---- driver-side metrics (k_metrics.hip) ------------------------------------
 // evaluate (traffic_triple_comparison.m:194-202): out2 = {sum (X(mask)-gt)^2,
-// sum gt^2}; mask may be null (X and gt paired elementwise).  scratch_i64:
+// sum gt^2}; mask may be null (X and gt paired elementwise, m == n); gt is
+// read only below m (a mask with more true entries than m is reported by the
+// caller through *total).  scratch_i64:
 // evaluate_blocks(n) + 1 entries; part: 2*evaluate_blocks(n) doubles; *total
 // receives nnz(mask) (untouched without a mask)
 int64_t evaluate_blocks(int64_t n);
-void launch_evaluate(const double* X, const double* gt, const uint8_t* mask, int64_t n,
+void launch_evaluate(const double* X, const double* gt, int64_t m, const uint8_t* mask, int64_t n,
                      int64_t* scratch_i64, double* part, double* out2, int64_t* total,
                      hipStream_t st);
 // quality_ybz: per-frame psnr/ssim of n1 x n2 x nf tensors; win = the
