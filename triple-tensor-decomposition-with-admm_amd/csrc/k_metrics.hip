@@ -86,27 +86,31 @@ __global__ __launch_bounds__(EV_THREADS) void k_mask_count(const uint8_t* __rest
     if (lane == 0) cnt[gw] = c;
 }
 
-// pass 2: exclusive scan of the chunk counts (one block, sequential carry)
+// pass 2: exclusive scan of the chunk counts in one block: thread t owns
+// the contiguous run [t*per, (t+1)*per), sums it, one block scan of the 256
+// run totals, then each run is rewritten with its offset (integers: exact)
 __global__ __launch_bounds__(EV_THREADS) void k_scan_counts(int64_t* __restrict__ cnt, int nb,
                                                             int64_t* __restrict__ total) {
     __shared__ int64_t sh[EV_THREADS];
-    int64_t carry = 0;
-    for (int b0 = 0; b0 < nb; b0 += EV_THREADS) {
-        const int b = b0 + (int)threadIdx.x;
-        const int64_t v = b < nb ? cnt[b] : 0;
-        sh[threadIdx.x] = v;
+    const int per = (nb + EV_THREADS - 1) / EV_THREADS;
+    const int b0 = (int)threadIdx.x * per, b1 = min(nb, b0 + per);
+    int64_t run = 0;
+    for (int b = b0; b < b1; ++b) run += cnt[b];
+    sh[threadIdx.x] = run;
+    __syncthreads();
+    for (int off = 1; off < EV_THREADS; off <<= 1) {  // Hillis-Steele inclusive
+        const int64_t add = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
         __syncthreads();
-        for (int off = 1; off < EV_THREADS; off <<= 1) {  // Hillis-Steele inclusive
-            const int64_t add = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += add;
-            __syncthreads();
-        }
-        if (b < nb) cnt[b] = carry + sh[threadIdx.x] - v;
-        carry += sh[EV_THREADS - 1];
+        sh[threadIdx.x] += add;
         __syncthreads();
     }
-    if (threadIdx.x == 0) *total = carry;
+    int64_t acc = sh[threadIdx.x] - run;
+    for (int b = b0; b < b1; ++b) {
+        const int64_t v = cnt[b];
+        cnt[b] = acc;
+        acc += v;
+    }
+    if (threadIdx.x == EV_THREADS - 1) *total = sh[EV_THREADS - 1];
 }
 
 // pass 3 (mask): sum (X(p) - gt(k))^2 and gt(k)^2 over the true positions p,
@@ -303,23 +307,28 @@ __global__ __launch_bounds__(256) void k_frame_sqdiff(const double* __restrict__
     if (threadIdx.x == 0) part[f * gridDim.x + blockIdx.x] = t;
 }
 
-// per frame: psnr(f) = 10 log10(255^2 / (sqsum/npix)); ssim(f) = mean2(map)
-// (-Inf when the frame is smaller than the window, ssim_index.m nargin == 2)
-__global__ void k_quality_finish(const double* __restrict__ sqpart, int nsq,
-                                 const double* __restrict__ sspart, int nss, int64_t nf,
-                                 double npix, double nmap, int small, double* __restrict__ psnr,
-                                 double* __restrict__ ssim) {
-    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= nf) return;
-    double a = 0.0;
-    for (int b = 0; b < nsq; ++b) a += sqpart[f * nsq + b];
-    psnr[f] = 10.0 * log10(255.0 * 255.0 / (a / npix));
-    if (small) {
-        ssim[f] = -INFINITY;
-    } else {
-        double s = 0.0;
-        for (int b = 0; b < nss; ++b) s += sspart[f * nss + b];
-        ssim[f] = s / nmap;
+// per frame (one wave each; lane-strided partial sums, then a fixed xor
+// tree: deterministic): psnr(f) = 10 log10(255^2 / (sqsum/npix));
+// ssim(f) = mean2(map) (-Inf when the frame is smaller than the window,
+// ssim_index.m nargin == 2)
+__global__ __launch_bounds__(64) void k_quality_finish(const double* __restrict__ sqpart, int nsq,
+                                                       const double* __restrict__ sspart, int nss,
+                                                       double npix, double nmap, int small,
+                                                       double* __restrict__ psnr,
+                                                       double* __restrict__ ssim) {
+    const int64_t f = blockIdx.x;
+    const int lane = threadIdx.x;
+    double a = 0.0, s = 0.0;
+    for (int b = lane; b < nsq; b += 64) a += sqpart[f * nsq + b];
+    for (int b = lane; b < nss; b += 64) s += sspart[f * nss + b];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        s += __shfl_xor(s, off);
+    }
+    if (lane == 0) {
+        psnr[f] = 10.0 * log10(255.0 * 255.0 / (a / npix));
+        ssim[f] = small ? -INFINITY : s / nmap;
     }
 }
 
@@ -327,6 +336,8 @@ void launch_quality(const double* X, const double* Y, int64_t n1, int64_t n2, in
                     const double* win, double C1, double C2, double* scratch, double* psnr,
                     double* ssim, hipStream_t st) {
     const int64_t fsz = n1 * n2;
+    // frames run on grid y/z (at most 65535 on gfx950)
+    if (nf > 65535) throw Error(TRITD_ERR_ARG, "quality_ybz: at most 65535 frames per call");
     const int nsq = (int)cdiv(fsz, SQ_CHUNK);
     double* sqpart = scratch;
     double* sspart = scratch + (size_t)nsq * nf;
@@ -342,8 +353,8 @@ void launch_quality(const double* X, const double* Y, int64_t n1, int64_t n2, in
         TRITD_CHECK_LAUNCH();
     }
     const double nmap = small ? 1.0 : (double)((n1 - (QW - 1)) * (n2 - (QW - 1)));
-    hipLaunchKernelGGL(k_quality_finish, dim3((unsigned)cdiv(nf, 64)), dim3(64), 0, st, sqpart, nsq,
-                       sspart, nss, nf, (double)fsz, nmap, (int)small, psnr, ssim);
+    hipLaunchKernelGGL(k_quality_finish, dim3((unsigned)nf), dim3(64), 0, st, sqpart, nsq, sspart,
+                       nss, (double)fsz, nmap, (int)small, psnr, ssim);
     TRITD_CHECK_LAUNCH();
 }
 
