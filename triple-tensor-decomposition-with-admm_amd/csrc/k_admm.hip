@@ -670,6 +670,7 @@ __global__ __launch_bounds__(256) void k_reduce_pairs(const double* __restrict__
     if (stop && *stop) return;
     __shared__ double sx[256], sy[256];
     double x = 0.0, y = 0.0;
+#pragma unroll 8  // loads batched; the sums keep their sequential order
     for (int b = threadIdx.x; b < n; b += 256) {
         x += p[2 * b];
         y += p[2 * b + 1];
@@ -730,6 +731,7 @@ __global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict_
     if (ctrl[0]) return;
     __shared__ double sx[256], sy[256];
     double x = 0.0, y = 0.0;
+#pragma unroll 8  // loads batched; the sums keep their sequential order
     for (int b = threadIdx.x; b < n; b += 256) {
         x += p[2 * b];
         y += p[2 * b + 1];

@@ -95,6 +95,7 @@ __global__ __launch_bounds__(EV_THREADS) void k_scan_counts(int64_t* __restrict_
     const int per = (nb + EV_THREADS - 1) / EV_THREADS;
     const int b0 = (int)threadIdx.x * per, b1 = min(nb, b0 + per);
     int64_t run = 0;
+#pragma unroll 16  // one block: batch the loads (latency-bound otherwise)
     for (int b = b0; b < b1; ++b) run += cnt[b];
     sh[threadIdx.x] = run;
     __syncthreads();
@@ -105,6 +106,7 @@ __global__ __launch_bounds__(EV_THREADS) void k_scan_counts(int64_t* __restrict_
         __syncthreads();
     }
     int64_t acc = sh[threadIdx.x] - run;
+#pragma unroll 16
     for (int b = b0; b < b1; ++b) {
         const int64_t v = cnt[b];
         cnt[b] = acc;
