@@ -46,7 +46,10 @@ namespace tritd {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-static constexpr int K5_WAVES = 4;
+#ifndef K5_NWAVES
+#define K5_NWAVES 4  // waves per workgroup (tiles4 group padding assumes a multiple of 4)
+#endif
+static constexpr int K5_WAVES = K5_NWAVES;
 #ifndef K5_NT
 #define K5_NT 0  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores
 #endif
