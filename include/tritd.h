@@ -301,14 +301,16 @@ tritd_status tritd_build_design_f64(char which, const double* P, const double* Q
  * norm(gt(:)).  X has n elements; mask is n bytes (MATLAB logical, nonzero =
  * true) or NULL for true(size(X)); gt holds m = nnz(mask) elements in
  * column-major order of the true positions (m = n without a mask) — a
- * mismatch fails like MATLAB's "Arrays have incompatible sizes".  */
+ * mismatch fails like MATLAB's "Arrays have incompatible sizes" (gt is never
+ * read past m).  The device variant takes a mask at any byte alignment.  */
 tritd_status tritd_evaluate_f64(const double* X, int64_t n, const double* gt, int64_t m,
                                 const uint8_t* mask, double* rmse, double* nrmse);
 /* quality_ybz(imagery1, imagery2) (other_methods/Low-rank-.../quality_ybz.m:1-33):
  * mean over the nf frames (n1 x n2 each; trailing dims folded into nf) of
  * psnr_index = 10*log10(255^2/mse(x-y)) and ssim_index (Gaussian 11x11
  * window, sigma 1.5, K = [0.01 0.03], L = 255, 'valid' map; -Inf for frames
- * smaller than 11x11).  psnr_frames / ssim_frames (nf each) may be NULL. */
+ * smaller than 11x11).  psnr_frames / ssim_frames (nf each) may be NULL.
+ * nf <= 65535 per call (TRITD_ERR_ARG beyond). */
 tritd_status tritd_quality_f64(const double* X1, const double* X2, int64_t n1, int64_t n2,
                                int64_t nf, double* psnr, double* ssim, double* psnr_frames,
                                double* ssim_frames);
