@@ -78,8 +78,21 @@ enum { TRITD_MODEL_CP = 0, TRITD_MODEL_QI = 1 };
  * Default: stdout.  MEX gateways install mexPrintf here. */
 typedef void (*tritd_print_fn)(const char* line, void* user);
 
+/* Warning flags (bitmask).  Not errors: the call succeeded and its outputs
+ * are valid, but they may differ from the reference's beyond rounding.
+ * TRITD_FLAG_PINV_TOL: an R x R ridge Gram's smallest pivot came within 1e3x
+ * of MATLAB's pinv tolerance max(size)*eps(max sigma)
+ * (triple_decomp_ADMM.m:78,86,93; triple_decomp_ALS.m:27,32,37): pinv could
+ * have truncated singular values there, the GPU's inverse does not. */
+enum { TRITD_FLAG_PINV_TOL = 1u };
+
 const char* tritd_version(void);
 const char* tritd_last_error(void);
+/* TRITD_FLAG_* of the last one-shot solve on this thread (tritd_admm_*,
+ * tritd_admm_sharded_virtual_f64, tritd_als_*, tritd_ncvx_f64; OR over the
+ * shards of a device set); 0 after a call that raised none, and after any
+ * failed libtritd call. */
+uint32_t tritd_last_flags(void);
 void tritd_set_print_callback(tritd_print_fn fn, void* user);
 /* Number of visible gfx950 devices (0 on a host without a GPU). */
 tritd_status tritd_device_count(int32_t* count);
@@ -177,6 +190,8 @@ tritd_status tritd_session_counters(tritd_session* s, int64_t* dense_tiles_total
  * tile (2 = E read + written; 3 = E^(k), E^(k-1) read + E^(k+1) written). */
 tritd_status tritd_session_k5_profile(tritd_session* s, int32_t* dense_streams,
                                       int32_t* slot_accesses);
+/* TRITD_FLAG_* raised by this session's solves so far (read at each sync). */
+tritd_status tritd_session_flags(tritd_session* s, uint32_t* flags);
 void tritd_session_destroy(tritd_session* s);
 
 /* ---------------------------------------------------------------------------
@@ -262,6 +277,7 @@ tritd_status tritd_als_session_get(tritd_als_session* s, double* A, double* B, d
 tritd_status tritd_als_session_set_timing(tritd_als_session* s, int32_t enable);
 tritd_status tritd_als_session_kernel_ms(tritd_als_session* s, double* fit_ms, double* mode3_ms,
                                          double* iteration_ms, int32_t* samples);
+tritd_status tritd_als_session_flags(tritd_als_session* s, uint32_t* flags);
 void tritd_als_session_destroy(tritd_als_session* s);
 /* Single-GPU rehearsal of the sharded ALS (virtual shards, as above). */
 tritd_status tritd_als_sharded_virtual_f64(const double* X, int64_t n1, int64_t n2, int64_t n3,
@@ -310,7 +326,7 @@ tritd_status tritd_evaluate_f64(const double* X, int64_t n, const double* gt, in
  * psnr_index = 10*log10(255^2/mse(x-y)) and ssim_index (Gaussian 11x11
  * window, sigma 1.5, K = [0.01 0.03], L = 255, 'valid' map; -Inf for frames
  * smaller than 11x11).  psnr_frames / ssim_frames (nf each) may be NULL.
- * nf <= 65535 per call (TRITD_ERR_ARG beyond). */
+ * Any nf (launched in batches of 65535 frames). */
 tritd_status tritd_quality_f64(const double* X1, const double* X2, int64_t n1, int64_t n2,
                                int64_t nf, double* psnr, double* ssim, double* psnr_frames,
                                double* ssim_frames);

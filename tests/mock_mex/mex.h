@@ -36,6 +36,7 @@ mxArray* mxCreateNumericArray(mwSize, const mwSize*, mxClassID, mxComplexity);
 mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
 void mxDestroyArray(mxArray*);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...);
 int mexPrintf(const char* fmt, ...);
 int mexAtExit(void (*fn)(void));
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]);

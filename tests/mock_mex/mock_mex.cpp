@@ -70,6 +70,16 @@ void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) {
     va_end(ap);
     throw MockMexError{id, buf};
 }
+// MATLAB prints "Warning: <msg>" and returns; the mock records it with the
+// printed text
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_printed += std::string("Warning [") + id + "]: " + buf + "\n";
+}
 int mexPrintf(const char* fmt, ...) {
     char buf[1024];
     va_list ap;

@@ -116,3 +116,30 @@ def test_quality_edge_cases(tritd):
     assert p == pytest.approx(20 * np.log10(255.0), rel=1e-14) and s == -np.inf
     p, s = tritd.quality_ybz(np.ones((12, 12, 1)), np.ones((12, 12, 1)))
     assert p == np.inf and s == 1.0
+
+
+def test_quality_more_frames_than_one_launch(tritd, orc):
+    """quality_ybz.m folds every trailing dimension into frames with no limit;
+    the kernels launch frames in batches of 65535 (grid y/z), so 65535 + 2500
+    frames cross a batch boundary.  Frames on both sides are checked against
+    the oracle, and the batch-seam frames against a single-batch call."""
+    nf = 65535 + 2500
+    rng = np.random.default_rng(8)
+    X = np.asfortranarray(rng.uniform(0, 255, (12, 11, nf)))
+    Y = np.asfortranarray(np.clip(X + rng.normal(0, 9, X.shape), 0, 255))
+    p, s, pf, sf = tritd.quality_ybz(X, Y, per_frame=True)
+    for f in (0, 1, 65533, 65534, 65535, 65536, nf - 1):
+        assert pf[f] == pytest.approx(orc.psnr_index(X[:, :, f], Y[:, :, f]), rel=1e-12)
+        assert sf[f] == pytest.approx(orc.ssim_index(X[:, :, f], Y[:, :, f]), rel=1e-11)
+    lo, hi = 65535 - 100, 65535 + 100
+    _, _, pf2, sf2 = tritd.quality_ybz(X[:, :, lo:hi], Y[:, :, lo:hi], per_frame=True)
+    np.testing.assert_array_equal(pf[lo:hi], pf2)
+    np.testing.assert_array_equal(sf[lo:hi], sf2)
+    assert p == pytest.approx(np.mean(pf), rel=1e-12) and s == pytest.approx(np.mean(sf), rel=1e-12)
+
+
+def test_unfold_more_matrices_than_one_launch(tritd, orc):
+    """unfold(X, 2) transposes n3 matrices (one per grid z); n3 > 65535 runs
+    in batches."""
+    X = np.asfortranarray(np.random.default_rng(9).standard_normal((3, 5, 70000)))
+    np.testing.assert_array_equal(tritd.unfold(X, 2), orc.unfold(X, 2))

@@ -235,3 +235,17 @@ def test_design_matrices_bit_exact(tritd, orc, r):
     np.testing.assert_array_equal(tritd.buildF(B, C), orc.buildF(B, C))
     np.testing.assert_array_equal(tritd.buildG(A, C), orc.buildG(A, C))
     np.testing.assert_array_equal(tritd.buildH(A, B), orc.buildH(A, B))
+
+
+@pytest.mark.parametrize("name", ["g20x18x16_r10", "g24x22x20_r16"])
+def test_fp64_session_wide_rank_matches_golden(tritd, orc, name):
+    """fp64 sessions (the bench / one-process-per-GPU path) take r = 9..16 like
+    the one-shot solver."""
+    g = load_golden(name)
+    n1, n2, n3 = g["D"].shape
+    s = tritd.Session(g["r"], g["opts"], g["A0"], g["B0"], g["C0"], n1=n1, n2=n2, n3=n3,
+                      D=g["D"], device=0)
+    s.run(g["opts"]["maxIter"])
+    r = s.get()
+    s.close()
+    check_solution(orc, (r["A"], r["B"], r["C"], r["O"], r["errHist"], r["E"], r["k"]), g, g["k"])

@@ -289,8 +289,9 @@ void AlsSession::sync(int* done, int* stopped) {
     TRITD_HIP(hipSetDevice(device_));
     TRITD_HIP(hipStreamSynchronize(st_));
     if (!ev_.empty()) harvest_timing();
-    int ctrl[2];
-    TRITD_HIP(hipMemcpy(ctrl, ctrl_, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    int ctrl[3];
+    TRITD_HIP(hipMemcpy(ctrl, ctrl_, 3 * sizeof(int), hipMemcpyDeviceToHost));
+    if (ctrl[2]) flags_ |= TRITD_FLAG_PINV_TOL;  // a solve's pivot neared pinv's cutoff
     if (done) *done = ctrl[1];
     if (stopped) *stopped = ctrl[0];
 }

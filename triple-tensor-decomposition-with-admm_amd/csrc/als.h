@@ -28,6 +28,8 @@ class AlsSession {
 
     void run(int iters);
     void sync(int* done, int* stopped);
+    // TRITD_FLAG_* raised by the device so far (read at every sync)
+    uint32_t flags() const { return flags_; }
     void get(double* A, double* B, double* C, double* errHist, int* iters);
     // the progress line of :17-19 (every 5 iterations, unconditional in the
     // reference); quiet = no host synchronisation for it (benchmarks)
@@ -78,6 +80,7 @@ class AlsSession {
     DBuf X_, XT_, Wk_;  // X tile-major, X in TX order (K2), W = X x3 C^
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
     DBuf red0_, red1_, red2_, fitpart_, m3part_, sqpart_, errHist_;
+    uint32_t flags_ = 0;
     int* ctrl_ = nullptr;  // [0] stop, [1] errHist entries, [2] pinv-tolerance flag
     bool timing_ = false;
     std::vector<hipEvent_t> ev_;  // per timed iteration: 5 events

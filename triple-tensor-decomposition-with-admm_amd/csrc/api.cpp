@@ -17,12 +17,14 @@ using namespace tritd;
 
 namespace {
 thread_local std::string g_last_error;
+thread_local uint32_t g_last_flags = 0;  // TRITD_FLAG_* of the last one-shot solve
 tritd_print_fn g_print = nullptr;
 void* g_print_user = nullptr;
 std::mutex g_mutex;  // calls are not re-entrant (SURVEY.md §8b Threading)
 
 tritd_status fail(tritd_status s, const std::string& m) {
     g_last_error = m;
+    g_last_flags = 0;
     return s;
 }
 
@@ -242,6 +244,7 @@ void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t 
         ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr,
                    O ? static_cast<char*>(O) + i0 * es : nullptr,
                    E ? static_cast<char*>(E) + i0 * es : nullptr, n1, p == 0 ? errHist : nullptr, &k);
+        g_last_flags |= ss[p]->flags();
     }
     if (iters) *iters = k;
 }
@@ -291,6 +294,7 @@ void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, in
         TRITD_HIP(hipSetDevice(devs[p]));
         ss[p]->get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, p == 0 ? errHist : nullptr, &k);
         if (ncvx && O) ss[p]->get_O(O + ss[p]->geom().i0, n1);
+        g_last_flags |= ss[p]->flags();
     }
     if (iters) *iters = k;
 }
@@ -343,6 +347,7 @@ extern "C" {
 
 const char* tritd_version(void) { return "tritd-mi355x 0.2.0 (gfx950, fp64 r<=8, fp32 r<=16)"; }
 const char* tritd_last_error(void) { return g_last_error.c_str(); }
+uint32_t tritd_last_flags(void) { return g_last_flags; }
 
 void tritd_set_print_callback(tritd_print_fn fn, void* user) {
     g_print = fn;
@@ -363,6 +368,7 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
                             const double* C0, double* A, double* B, double* C, double* O,
                             double* E, double* errHist, int32_t* iters, int32_t device) {
     std::lock_guard<std::mutex> lk(g_mutex);
+    g_last_flags = 0;
     return guarded([&] {
         check_opts(opts);
         check_dims(n1, n2, n3, r, true);  // fp64 ADMM: r <= 16 (r > 8 untuned)
@@ -378,6 +384,7 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
         s.run(o.maxIter);
         int k = 0;
         s.get(A, B, C, O, E, n1, errHist, &k);
+        g_last_flags |= s.flags();
         if (iters) *iters = k;
     });
 }
@@ -387,6 +394,7 @@ tritd_status tritd_admm_f32(const float* D, int64_t n1, int64_t n2, int64_t n3, 
                             const double* C0, double* A, double* B, double* C, float* O, float* E,
                             double* errHist, int32_t* iters, int32_t device) {
     std::lock_guard<std::mutex> lk(g_mutex);
+    g_last_flags = 0;
     return guarded([&] {
         check_opts(opts);
         check_dims(n1, n2, n3, r, true);
@@ -402,6 +410,7 @@ tritd_status tritd_admm_f32(const float* D, int64_t n1, int64_t n2, int64_t n3, 
         s.run(o.maxIter);
         int k = 0;
         s.get(A, B, C, O, E, n1, errHist, &k);
+        g_last_flags |= s.flags();
         if (iters) *iters = k;
     });
 }
@@ -415,7 +424,7 @@ tritd_status tritd_session_create(tritd_session** out, int32_t device, const voi
         need(out, "out");
         *out = nullptr;
         check_opts(opts);
-        check_dims(n1, n2, n3, r, (flags & TRITD_SESSION_F32) != 0);
+        check_dims(n1, n2, n3, r, true);  // ADMM, fp64 or fp32: r <= 16
         need(D, "D"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
         if (i0 < 0 || i1 > n1 || i0 >= i1) throw Error(TRITD_ERR_ARG, "bad shard range");
         if (ldD < i1 - i0) throw Error(TRITD_ERR_ARG, "ldD smaller than the shard");
@@ -538,6 +547,14 @@ tritd_status tritd_session_k5_profile(tritd_session* s, int32_t* dense_streams,
     });
 }
 
+tritd_status tritd_session_flags(tritd_session* s, uint32_t* flags) {
+    return guarded([&] {
+        need(s, "session");
+        need(flags, "flags");
+        *flags = reinterpret_cast<Session*>(s)->flags();
+    });
+}
+
 void tritd_session_destroy(tritd_session* s) { delete reinterpret_cast<Session*>(s); }
 
 tritd_status tritd_comm_unique_id(void* id128) {
@@ -581,6 +598,7 @@ tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t
                                             double* A, double* B, double* C, double* O, double* E,
                                             double* errHist, int32_t* iters, int32_t device) {
     std::lock_guard<std::mutex> lk(g_mutex);
+    g_last_flags = 0;
     return guarded([&] {
         check_opts(opts);
         check_dims(n1, n2, n3, r, true);  // fp64 ADMM: r <= 16 (r > 8 untuned)
@@ -621,6 +639,7 @@ tritd_status tritd_als_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, 
                            const double* C0, double* A, double* B, double* C, double* errHist,
                            int32_t* iters, int32_t device) {
     std::lock_guard<std::mutex> lk(g_mutex);
+    g_last_flags = 0;
     return guarded([&] {
         check_als_opts(opts);
         check_dims(n1, n2, n3, r);
@@ -636,6 +655,7 @@ tritd_status tritd_als_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, 
         s.run(maxIter);
         int k = 0;
         s.get(A, B, C, errHist, &k);
+        g_last_flags |= s.flags();
         if (iters) *iters = k;
     });
 }
@@ -646,6 +666,7 @@ tritd_status tritd_als_sharded_virtual_f64(const double* X, int64_t n1, int64_t 
                                            double* A, double* B, double* C, double* errHist,
                                            int32_t* iters, int32_t device) {
     std::lock_guard<std::mutex> lk(g_mutex);
+    g_last_flags = 0;
     return guarded([&] {
         check_als_opts(opts);
         check_dims(n1, n2, n3, r);
@@ -665,6 +686,7 @@ tritd_status tritd_ncvx_f64(const double* X, int64_t n1, int64_t n2, int64_t n3,
                            const double* B0, const double* C0, double* A, double* B, double* C,
                            double* O, double* errHist, int32_t* iters, int32_t device) {
     std::lock_guard<std::mutex> lk(g_mutex);
+    g_last_flags = 0;
     return guarded([&] {
         check_dims(n1, n2, n3, r);
         need(X, "X"); need(A0, "A0"); need(B0, "B0"); need(C0, "C0");
@@ -684,6 +706,7 @@ tritd_status tritd_ncvx_f64(const double* X, int64_t n1, int64_t n2, int64_t n3,
         int k = 0;
         s.get(A, B, C, errHist, &k);
         s.get_O(O, n1);
+        g_last_flags |= s.flags();
         if (iters) *iters = k;
     });
 }
@@ -753,6 +776,14 @@ tritd_status tritd_als_session_kernel_ms(tritd_als_session* s, double* fit_ms, d
         int n = 0;
         reinterpret_cast<AlsSession*>(s)->kernel_ms(fit_ms, mode3_ms, iteration_ms, &n);
         if (samples) *samples = n;
+    });
+}
+
+tritd_status tritd_als_session_flags(tritd_als_session* s, uint32_t* flags) {
+    return guarded([&] {
+        need(s, "session");
+        need(flags, "flags");
+        *flags = reinterpret_cast<AlsSession*>(s)->flags();
     });
 }
 

@@ -46,10 +46,11 @@ namespace tritd {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-#ifndef K5_NWAVES
-#define K5_NWAVES 4  // waves per workgroup (tiles4 group padding assumes a multiple of 4)
-#endif
-static constexpr int K5_WAVES = K5_NWAVES;
+// Waves per workgroup: exactly one group of 4 ij-tiles (common.h: the TM
+// layout interleaves groups of 4 and pads tiles4 to a multiple of 4, so a
+// wider workgroup would stream past the allocation; 8 waves measured no
+// faster).
+static constexpr int K5_WAVES = 4;
 #ifndef K5_NT
 #define K5_NT 0  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores
 #endif
@@ -357,6 +358,12 @@ void k5_fused(K5Args a) {
     };
     __shared__ double csm[K5_WAVES][96];
     double* cs = csm[wid];
+    // every __shared__ array of this kernel, in bytes (160 KiB per CU; RP =
+    // 256 at one wave per SIMD is the largest: ~147 KB)
+    constexpr size_t LDS_BYTES =
+        sizeof(double) * (2 * RP * 16 + 2 * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
+                          2 * K5_WAVES + (K5_KRLDS ? K5_WAVES * KS * 64 : 0));
+    static_assert(LDS_BYTES <= 160 * 1024, "k5_fused: LDS over the 160 KiB of a CU");
     auto load = [&](int64_t tt, Regs& nx) {
         const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
 #pragma unroll

@@ -162,6 +162,12 @@ void k5_f32(K5Args32 a) {
     __shared__ float csm[K5W][128];     // per-wave compact-E slot image
     float* ts = tsm[wid];
     float* cs = csm[wid];
+    // every __shared__ array of this kernel (sC, tsm, csm, the W exchange wl,
+    // red), in bytes: at most the 160 KiB of a CU
+    static_assert(sizeof(float) * (2 * 16 * LDC + K5W * 16 * 17 + K5W * 128 + K5W * (RP * 16 + 16)) +
+                          sizeof(double) * 2 * K5W <=
+                      160 * 1024,
+                  "k5_f32: LDS over the 160 KiB of a CU");
 
     // C^ slice of one t-tile: 16 rows x RP floats, loaded before the tile
     // prefetch, written to LDS after the tile's compute (in-order vmcnt)

@@ -338,26 +338,35 @@ void launch_quality(const double* X, const double* Y, int64_t n1, int64_t n2, in
                     const double* win, double C1, double C2, double* scratch, double* psnr,
                     double* ssim, hipStream_t st) {
     const int64_t fsz = n1 * n2;
-    // frames run on grid y/z (at most 65535 on gfx950)
-    if (nf > 65535) throw Error(TRITD_ERR_ARG, "quality_ybz: at most 65535 frames per call");
     const int nsq = (int)cdiv(fsz, SQ_CHUNK);
     double* sqpart = scratch;
     double* sspart = scratch + (size_t)nsq * nf;
-    hipLaunchKernelGGL(k_frame_sqdiff, dim3(nsq, (unsigned)nf), dim3(256), 0, st, X, Y, fsz, sqpart);
-    TRITD_CHECK_LAUNCH();
     const bool small = n1 < QW || n2 < QW;
-    int nss = 0;
-    if (!small) {
-        const unsigned gx = (unsigned)cdiv(n1 - (QW - 1), QT), gy = (unsigned)cdiv(n2 - (QW - 1), QT);
-        nss = (int)(gx * gy);
-        hipLaunchKernelGGL(k_ssim_tiles, dim3(gx, gy, (unsigned)nf), dim3(QT * QT), 0, st, X, Y, n1,
-                           n2, win, C1, C2, sspart);
+    const unsigned gx = small ? 0u : (unsigned)cdiv(n1 - (QW - 1), QT);
+    const unsigned gy = small ? 0u : (unsigned)cdiv(n2 - (QW - 1), QT);
+    const int nss = (int)(gx * gy);
+    const double nmap = small ? 1.0 : (double)((n1 - (QW - 1)) * (n2 - (QW - 1)));
+    // frames run on grid y/z (at most 65535 per launch on gfx950): batches of
+    // QF frames, each batch's pointers offset to its first frame
+    constexpr int64_t QF = 65535;
+    for (int64_t f0 = 0; f0 < nf; f0 += QF) {
+        const int64_t nb = nf - f0 < QF ? nf - f0 : QF;
+        const double* Xb = X + f0 * fsz;
+        const double* Yb = Y + f0 * fsz;
+        double* sqb = sqpart + (size_t)nsq * f0;
+        double* ssb = sspart + (size_t)nss * f0;
+        hipLaunchKernelGGL(k_frame_sqdiff, dim3(nsq, (unsigned)nb), dim3(256), 0, st, Xb, Yb, fsz,
+                           sqb);
+        TRITD_CHECK_LAUNCH();
+        if (!small) {
+            hipLaunchKernelGGL(k_ssim_tiles, dim3(gx, gy, (unsigned)nb), dim3(QT * QT), 0, st, Xb,
+                               Yb, n1, n2, win, C1, C2, ssb);
+            TRITD_CHECK_LAUNCH();
+        }
+        hipLaunchKernelGGL(k_quality_finish, dim3((unsigned)nb), dim3(64), 0, st, sqb, nsq, ssb,
+                           nss, (double)fsz, nmap, (int)small, psnr + f0, ssim + f0);
         TRITD_CHECK_LAUNCH();
     }
-    const double nmap = small ? 1.0 : (double)((n1 - (QW - 1)) * (n2 - (QW - 1)));
-    hipLaunchKernelGGL(k_quality_finish, dim3((unsigned)nf), dim3(64), 0, st, sqpart, nsq, sspart,
-                       nss, (double)fsz, nmap, (int)small, psnr, ssim);
-    TRITD_CHECK_LAUNCH();
 }
 
 size_t quality_scratch(int64_t n1, int64_t n2, int64_t nf) {

@@ -307,7 +307,15 @@ __global__ __launch_bounds__(256) void k_transpose_tall(const double* __restrict
 
 void launch_transpose_batched(const double* in, double* out, int64_t rows, int64_t cols,
                               int64_t batch, hipStream_t st) {
-    if (batch > 65535) throw Error(TRITD_ERR_ARG, "transpose batch too large");
+    if (batch > 65535) {  // grid z holds at most 65535: batches of matrices
+        const int64_t mat = rows * cols;
+        for (int64_t b0 = 0; b0 < batch; b0 += 65535)
+            launch_transpose_batched(in + b0 * mat, out + b0 * mat, rows, cols,
+                                     batch - b0 < 65535 ? batch - b0 : 65535, st);
+        return;
+    }
+    if (cdiv(rows, TT) > INT32_MAX || cdiv(cols, TT) > 65535)
+        throw Error(TRITD_ERR_ARG, "unfold: matrix too large for one transpose launch");
     constexpr int TR = 32, TC = 128;
     if (batch == 1 && rows % TR == 0 && cols % TC == 0 && rows >= 64 * cols &&
         (((uintptr_t)in | (uintptr_t)out) & 15) == 0 && (rows / TR) * (cols / TC) < (1LL << 31)) {

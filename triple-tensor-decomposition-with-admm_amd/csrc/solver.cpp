@@ -740,6 +740,7 @@ void Session::sync(int* done, int* stopped) {
     if (!ev_.empty()) harvest_timing();
     int ctrl[3];
     TRITD_HIP(hipMemcpy(ctrl, ctrl_, 3 * sizeof(int), hipMemcpyDeviceToHost));
+    if (ctrl[2]) flags_ |= TRITD_FLAG_PINV_TOL;  // a solve's pivot neared pinv's cutoff
     if (done) *done = ctrl[1];
     if (stopped) *stopped = ctrl[0];
 }

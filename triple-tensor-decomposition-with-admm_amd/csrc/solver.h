@@ -55,6 +55,8 @@ class Session {
     // Enqueue iterations (full collective schedule; used without a virtual group)
     void run(int iters);
     void sync(int* done, int* stopped);
+    // TRITD_FLAG_* raised by the device so far (read at every sync)
+    uint32_t flags() const { return flags_; }
     // O, E: double, or float for an fp32 session
     void get(double* A, double* B, double* C, void* O, void* E, int64_t ldOE, double* errHist,
              int* iters);
@@ -161,6 +163,7 @@ class Session {
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;
     DBuf errHist_, errL_, errO_;
+    uint32_t flags_ = 0;
     int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag, then DENSE_SLOTS u64 dense-E counters
     unsigned long long* dense_tiles() const {
         return reinterpret_cast<unsigned long long*>(ctrl_ + 4);

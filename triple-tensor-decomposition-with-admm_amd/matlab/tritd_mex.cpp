@@ -116,6 +116,16 @@ void need_double(const mxArray* a, const char* what) {
     if (!mxIsDouble(a) || mxIsComplex(a)) fail("tritd:class", std::string(what) + " must be real double");
 }
 
+// TRITD_FLAG_PINV_TOL of the solve that just returned: a MATLAB warning (the
+// outputs are still returned)
+void warn_flags() {
+    if (tritd_last_flags() & TRITD_FLAG_PINV_TOL)
+        mexWarnMsgIdAndTxt("tritd:pinvTolerance",
+                           "a Gram's smallest pivot came within 1e3x of pinv's tolerance; pinv "
+                           "could have truncated there (results may differ from the reference "
+                           "beyond rounding)");
+}
+
 std::string status_msg(tritd_status s) {
     return std::string("libtritd: ") + tritd_last_error() + " (status " + std::to_string((int)s) + ")";
 }
@@ -161,6 +171,7 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         for (mxArray* x : {A, B, C, O, E, eh}) mxDestroyArray(x);
         fail(st == TRITD_ERR_OPTS ? "MATLAB:nonExistentField" : "tritd:solver", status_msg(st));
     }
+    warn_flags();
     mxSetM(eh, (mwSize)k);  // errHist = errHist(1:k)  (triple_decomp_ADMM.m:68)
     mxArray* outs[6] = {A, B, C, O, eh, E};
     for (int q = 0; q < 6; ++q) {
@@ -223,6 +234,7 @@ void do_als(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         for (mxArray* x : {A, B, C, eh}) mxDestroyArray(x);
         fail(st == TRITD_ERR_OPTS ? "MATLAB:nonExistentField" : "tritd:solver", status_msg(st));
     }
+    warn_flags();
     mxSetM(eh, (mwSize)k);  // errHist = errHist(1:k)  (triple_decomp_ALS.m:21)
     mxArray* outs[4] = {A, B, C, eh};
     for (int q = 0; q < 4; ++q) {
@@ -269,6 +281,7 @@ void do_ncvx(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         for (mxArray* x : {A, B, C, O, eh}) mxDestroyArray(x);
         fail("tritd:solver", status_msg(st));
     }
+    warn_flags();
     mxSetM(eh, (mwSize)k);  // errHist(1:k) on a break (test.m:66); maxIter entries otherwise
     mxArray* outs[5] = {A, B, C, O, eh};
     for (int q = 0; q < 5; ++q) {

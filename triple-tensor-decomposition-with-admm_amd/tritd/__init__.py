@@ -6,7 +6,7 @@ Import with the package directory on sys.path:
     import tritd
     A, B, C, O, errHist = tritd.triple_decomp_ADMM(D, r, opts)
 """
-from ._lib import LIB_PATH, TritdError, device_count, set_devices, set_printer, shutdown  # noqa: F401
+from ._lib import LIB_PATH, PinvToleranceWarning, TritdError, device_count, set_devices, set_printer, shutdown  # noqa: F401
 from .api import (  # noqa: F401
     AlsSession,
     Comm,

@@ -24,12 +24,20 @@ OPT_BITS = {"mu": OPT_MU, "rho": OPT_RHO, "lambda": OPT_LAMBDA, "lambda2": OPT_L
 MODELS = {"cp": 0, "qi": 1}  # opts.model: TRITD_MODEL_CP / TRITD_MODEL_QI (include/tritd.h)
 SESSION_D_ON_DEVICE = 1
 SESSION_F32 = 2
+FLAG_PINV_TOL = 1  # TRITD_FLAG_PINV_TOL (include/tritd.h)
 
 
 class TritdError(RuntimeError):
     def __init__(self, status, msg):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
         self.status = status
+
+
+class PinvToleranceWarning(UserWarning):
+    """TRITD_FLAG_PINV_TOL: a ridge Gram's smallest pivot came within 1e3x of
+    MATLAB's pinv tolerance (triple_decomp_ADMM.m:78,86,93), where pinv could
+    truncate singular values and the GPU's inverse does not — results may
+    differ from the reference's beyond rounding."""
 
 
 class Opts(C.Structure):
@@ -49,6 +57,9 @@ i32 = C.c_int32
 SIGNATURES = {
     "tritd_version": (C.c_char_p, []),
     "tritd_last_error": (C.c_char_p, []),
+    "tritd_last_flags": (C.c_uint32, []),
+    "tritd_session_flags": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
+    "tritd_als_session_flags": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
     "tritd_set_print_callback": (None, [PRINT_FN, vp]),
     "tritd_device_count": (C.c_int, [C.POINTER(i32)]),
     "tritd_admm_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp, vp, vp, vp, vp,
@@ -125,6 +136,21 @@ lib = _load()
 def check(status):
     if status != OK:
         raise TritdError(status, lib.tritd_last_error().decode(errors="replace"))
+
+
+def warn_flags(flags, where):
+    """Turn TRITD_FLAG_* bits into Python warnings (the call itself succeeded)."""
+    if flags & FLAG_PINV_TOL:
+        import warnings
+        warnings.warn(f"{where}: a Gram's smallest pivot came within 1e3x of MATLAB's pinv "
+                      "tolerance; pinv could have truncated there (results may differ from the "
+                      "reference beyond rounding)", PinvToleranceWarning, stacklevel=3)
+
+
+def check_flags(status, where):
+    """check() for the one-shot solvers, then warn on tritd_last_flags()."""
+    check(status)
+    warn_flags(lib.tritd_last_flags(), where)
 
 
 def device_count():

@@ -31,7 +31,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import TritdError, check, lib
+from ._lib import PinvToleranceWarning, TritdError, check, check_flags, lib
 
 REQUIRED = ("mu", "rho", "lambda", "lambda2", "maxIter", "tol", "disp")
 
@@ -139,14 +139,14 @@ def triple_decomp_ADMM(D, r, opts, A0=None, B0=None, C0=None, *, device=-1, retu
     errHist = np.zeros(max(o.maxIter, 1))
     k = _lib.i32(0)
     if virtual_shards and virtual_shards > 1:
-        check(lib.tritd_admm_sharded_virtual_f64(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0),
+        check_flags(lib.tritd_admm_sharded_virtual_f64(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0),
                                                  _ptr(B0), _ptr(C0), int(virtual_shards), _ptr(A),
                                                  _ptr(B), _ptr(Cf), _ptr(O), _ptr(E),
-                                                 _ptr(errHist), C.byref(k), int(device)))
+                                                 _ptr(errHist), C.byref(k), int(device)), "triple_decomp_ADMM")
     else:
-        check(lib.tritd_admm_f64(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+        check_flags(lib.tritd_admm_f64(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
                                  _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), _ptr(errHist),
-                                 C.byref(k), int(device)))
+                                 C.byref(k), int(device)), "triple_decomp_ADMM")
     errHist = errHist[: k.value].copy()  # :68 errHist = errHist(1:k)
     out = [A, B, Cf, O, errHist]
     if return_E:
@@ -171,9 +171,9 @@ def _admm_f32(D, r, o, opts, A0, B0, C0, device, return_E, return_iters):
     E = np.zeros((n1, n2, n3), order="F", dtype=np.float32)
     errHist = np.zeros(max(o.maxIter, 1))
     k = _lib.i32(0)
-    check(lib.tritd_admm_f32(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+    check_flags(lib.tritd_admm_f32(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
                              _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), _ptr(errHist),
-                             C.byref(k), int(device)))
+                             C.byref(k), int(device)), "triple_decomp_ADMM")
     out = [A, B, Cf, O, errHist[: k.value].copy()]
     if return_E:
         out.append(E)
@@ -207,10 +207,10 @@ def triple_decomp_ncvx(X, r, rho, lam, gamma_A, epsilon, p, theta, maxIter, tol,
     O = np.zeros((n1, n2, n3), order="F")
     errHist = np.zeros(max(maxIter, 1))
     k = _lib.i32(0)
-    check(lib.tritd_ncvx_f64(_ptr(X), n1, n2, n3, r, float(rho), float(lam), float(gamma_A),
+    check_flags(lib.tritd_ncvx_f64(_ptr(X), n1, n2, n3, r, float(rho), float(lam), float(gamma_A),
                              float(epsilon), float(p), float(theta), maxIter, float(tol), _ptr(A0),
                              _ptr(B0), _ptr(C0), _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(errHist),
-                             C.byref(k), int(device)))
+                             C.byref(k), int(device)), "triple_decomp_ADMM_outlier")
     out = [A, B, Cf, O, errHist[: k.value].copy()]
     if return_iters:
         out.append(k.value)
@@ -265,14 +265,14 @@ def triple_decomp_ALS(X, r, opts, A0=None, B0=None, C0=None, *, device=-1, retur
     errHist = np.zeros(max(o.maxIter, 1))
     k = _lib.i32(0)
     if virtual_shards and virtual_shards > 1:
-        check(lib.tritd_als_sharded_virtual_f64(_ptr(X), n1, n2, n3, r, C.byref(o), _ptr(A0),
+        check_flags(lib.tritd_als_sharded_virtual_f64(_ptr(X), n1, n2, n3, r, C.byref(o), _ptr(A0),
                                                 _ptr(B0), _ptr(C0), int(virtual_shards), _ptr(A),
                                                 _ptr(B), _ptr(Cf), _ptr(errHist), C.byref(k),
-                                                int(device)))
+                                                int(device)), "triple_decomp_ALS")
     else:
-        check(lib.tritd_als_f64(_ptr(X), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
+        check_flags(lib.tritd_als_f64(_ptr(X), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
                                 _ptr(A), _ptr(B), _ptr(Cf), _ptr(errHist), C.byref(k),
-                                int(device)))
+                                int(device)), "triple_decomp_ALS")
     out = [A, B, Cf, errHist[: k.value].copy()]  # :21 errHist = errHist(1:k)
     if return_iters:
         out.append(k.value)
@@ -425,6 +425,12 @@ class Session:
         check(lib.tritd_session_sync(self._s, C.byref(d), C.byref(s)))
         return d.value, bool(s.value)
 
+    def flags(self):
+        """TRITD_FLAG_* raised so far (read at each sync)."""
+        f = C.c_uint32(0)
+        check(lib.tritd_session_flags(self._s, C.byref(f)))
+        return f.value
+
     def get(self):
         r, n1, n2, n3 = self.r, self.n1, self.n2, self.n3
         nl = self.i1 - self.i0
@@ -438,6 +444,7 @@ class Session:
         k = _lib.i32(0)
         fn = lib.tritd_session_get_f32 if self.f32 else lib.tritd_session_get
         check(fn(self._s, _ptr(A), _ptr(B), _ptr(Cf), _ptr(O), _ptr(E), nl, _ptr(eh), C.byref(k)))
+        _lib.warn_flags(self.flags(), "Session")
         return dict(A=A, B=B, C=Cf, O=O, E=E, errHist=eh[: k.value].copy(), k=k.value)
 
     def rre_parts(self, dX_ptr, ldX):
@@ -524,6 +531,12 @@ class AlsSession:
         check(lib.tritd_als_session_sync(self._s, C.byref(d), C.byref(s)))
         return d.value, bool(s.value)
 
+    def flags(self):
+        """TRITD_FLAG_* raised so far (read at each sync)."""
+        f = C.c_uint32(0)
+        check(lib.tritd_als_session_flags(self._s, C.byref(f)))
+        return f.value
+
     def get(self):
         r, n1, n2, n3 = self.r, self.n1, self.n2, self.n3
         A = np.zeros((n1, r, r), order="F")
@@ -532,6 +545,7 @@ class AlsSession:
         eh = np.zeros(max(self.maxIter, 1))
         k = _lib.i32(0)
         check(lib.tritd_als_session_get(self._s, _ptr(A), _ptr(B), _ptr(Cf), _ptr(eh), C.byref(k)))
+        _lib.warn_flags(self.flags(), "AlsSession")
         return dict(A=A, B=B, C=Cf, errHist=eh[: k.value].copy(), k=k.value)
 
     def set_timing(self, on=True):
@@ -580,4 +594,4 @@ __all__ = ["triple_decomp_ADMM", "triple_decomp_ADMM_outlier", "triple_decomp_AL
            "triple_decomp_ncvx",
            "make_als_opts", "evaluate", "quality_ybz", "triple_product", "unfold",
            "soft_threshold", "buildF", "buildG", "buildH", "Session", "Comm", "TritdError",
-           "make_opts", "initial_factors"]
+           "make_opts", "initial_factors", "PinvToleranceWarning"]
