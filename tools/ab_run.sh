@@ -1,0 +1,9 @@
+#!/bin/bash
+# parity subset with the in-tree lib, then an interleaved A/B of built variants
+#   bash tools/ab_run.sh "ab/base.so,ab/x.so" reps iters [pytest-target]
+set -uo pipefail
+mkdir -p gpurun_out/ab
+T=${4:-tests/test_gpu_parity.py}
+timeout -k 10 300 python -u -m pytest $T -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/par.log 2>&1
+rc=$?; tail -2 gpurun_out/ab/par.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python3 tools/ab_lib.py "$1" "$2" "$3"

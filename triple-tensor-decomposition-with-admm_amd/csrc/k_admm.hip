@@ -234,6 +234,11 @@ void k5_fused(K5Args a) {
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
     constexpr int LDC = RP + 16; // row stride of the [t][k] C^ slice (2*LDC = 32 mod 64: no bank conflicts)
+    // row stride of the [k][t] slice: odd, so the staging writes (32 lanes of
+    // one t, k = 0, 2, .., 62) fall on distinct banks (stride 16 put them all
+    // on one: 16-way conflicts, ~45 % of K5's LDS cycles); the L-operand
+    // reads then share one bank pair between two lanes (3 LDS cycles, not 2)
+    constexpr int SK = 17;
     const int lane = threadIdx.x & 63;
     // wave-uniform in SGPRs: every tile base below becomes scalar address math
     // (K5 is VALU-issue-bound)
@@ -249,9 +254,9 @@ void k5_fused(K5Args a) {
     // this lane's d2v slot of pair p in t-tile tt: tm_tile_base(tile, tt)/2 + 64p + lane
 
     // C^ rows of one t-tile, staged once per workgroup (double buffered):
-    //   sCT[k][16]  (L operand: C^(t0+l&15, 4s+(l>>4)))
+    //   sCT[k][SK]  (L operand: C^(t0+l&15, 4s+(l>>4)))
     //   sC [16][LDC] (W operand: C^(t0+4r+(l>>4), 16m+(l&15)))
-    __shared__ double sCT[2][RP * 16];
+    __shared__ double sCT[2][RP * SK];
     __shared__ double sC[2][16 * LDC];
     // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
     __shared__ double tsm[K5_WAVES][16 * 17];
@@ -284,8 +289,8 @@ void k5_fused(K5Args a) {
                 const int row = (2 * e) / RP, k = (2 * e) % RP;
                 sC[buf][row * LDC + k] = sv[q][0];
                 sC[buf][row * LDC + k + 1] = sv[q][1];
-                sCT[buf][k * 16 + row] = sv[q][0];
-                sCT[buf][(k + 1) * 16 + row] = sv[q][1];
+                sCT[buf][k * SK + row] = sv[q][0];
+                sCT[buf][(k + 1) * SK + row] = sv[q][1];
             }
         }
     };
@@ -361,7 +366,7 @@ void k5_fused(K5Args a) {
     // every __shared__ array of this kernel, in bytes (160 KiB per CU; RP =
     // 256 at one wave per SIMD is the largest: ~147 KB)
     constexpr size_t LDS_BYTES =
-        sizeof(double) * (2 * RP * 16 + 2 * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
+        sizeof(double) * (2 * RP * SK + 2 * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
                           2 * K5_WAVES + (K5_KRLDS ? K5_WAVES * KS * 64 : 0));
     static_assert(LDS_BYTES <= 160 * 1024, "k5_fused: LDS over the 160 KiB of a CU");
     auto load = [&](int64_t tt, Regs& nx) {
@@ -474,7 +479,7 @@ void k5_fused(K5Args a) {
                 for (int c = 0; c < K5_LSPLIT; ++c) lp[c] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int s = 0; s < KS; ++s)
-                    lp[s % K5_LSPLIT] = mfma4(cT[(4 * s + tg) * 16 + il], KR(s), lp[s % K5_LSPLIT]);
+                    lp[s % K5_LSPLIT] = mfma4(cT[(4 * s + tg) * SK + il], KR(s), lp[s % K5_LSPLIT]);
                 lacc = lp[0];
 #pragma unroll
                 for (int c = 1; c < K5_LSPLIT; ++c) lacc = lacc + lp[c];
@@ -482,7 +487,7 @@ void k5_fused(K5Args a) {
 #else
             if (!(K5_EXP & 1))
 #pragma unroll
-                for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * 16 + il], KR(s), lacc);
+                for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * SK + il], KR(s), lacc);
 #endif
             double En[4];
 #pragma unroll

@@ -36,6 +36,7 @@ void k_als_fit(AlsFitArgs a) {
     constexpr int KS = RP / 4;    // K-steps of the L MFMA
     constexpr int MT = RP / 16;   // k-tiles of W
     constexpr int LDC = RP + 16;  // padded row stride of the [t][k] slice
+    constexpr int SK = 17;        // odd [k][t] row stride: conflict-free staging writes (k_admm.hip)
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int il = lane & 15;
@@ -47,7 +48,7 @@ void k_als_fit(AlsFitArgs a) {
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
 
-    __shared__ double sCT[2][RP * 16];   // L operand  C^(t0 + l&15, 4s + l>>4)
+    __shared__ double sCT[2][RP * SK];   // L operand  C^(t0 + l&15, 4s + l>>4)
     __shared__ double sC[2][16 * LDC];   // W operand  C^(t0 + 4r + l>>4, 16m + l&15)
     constexpr int SP = 16 * RP / 2;
     constexpr int NS = (SP + 64 * FIT_WAVES - 1) / (64 * FIT_WAVES);
@@ -68,8 +69,8 @@ void k_als_fit(AlsFitArgs a) {
                 const int row = (2 * e) / RP, k = (2 * e) % RP;
                 sC[buf][row * LDC + k] = sv[q][0];
                 sC[buf][row * LDC + k + 1] = sv[q][1];
-                sCT[buf][k * 16 + row] = sv[q][0];
-                sCT[buf][(k + 1) * 16 + row] = sv[q][1];
+                sCT[buf][k * SK + row] = sv[q][0];
+                sCT[buf][(k + 1) * SK + row] = sv[q][1];
             }
         }
     };
@@ -119,7 +120,7 @@ void k_als_fit(AlsFitArgs a) {
         const double* cR = sC[buf];
         d4 lacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int s = 0; s < KS; ++s) lacc = als_mfma4(cT[(4 * s + tg) * 16 + il], kr[s], lacc);
+        for (int s = 0; s < KS; ++s) lacc = als_mfma4(cT[(4 * s + tg) * SK + il], kr[s], lacc);
         double xr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) xr[r] = cx.x[r >> 1][r & 1];
