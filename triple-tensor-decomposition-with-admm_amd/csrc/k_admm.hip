@@ -78,6 +78,9 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_EXP
 #define K5_EXP 0  // timing experiments only (tools/): drop parts of the t-tile work
 #endif
+#ifndef K5_PIPE
+#define K5_PIPE 1  // L of t-tile tt+1 computed during t-tile tt (triple-buffered C^ slices)
+#endif
 
 __device__ __forceinline__ double matlab_sign(double x) {
     // sign(): 1 / -1 / 0 (also for -0), NaN stays NaN; selects only, no
@@ -253,11 +256,19 @@ void k5_fused(K5Args a) {
     const int64_t ntt = a.ntt;
     // this lane's d2v slot of pair p in t-tile tt: tm_tile_base(tile, tt)/2 + 64p + lane
 
-    // C^ rows of one t-tile, staged once per workgroup (double buffered):
+    // C^ rows of one t-tile, staged once per workgroup:
     //   sCT[k][SK]  (L operand: C^(t0+l&15, 4s+(l>>4)))
     //   sC [16][LDC] (W operand: C^(t0+4r+(l>>4), 16m+(l&15)))
-    __shared__ double sCT[2][RP * SK];
-    __shared__ double sC[2][16 * LDC];
+    // PIPE: the L MFMAs of t-tile tt+1 run during t-tile tt, beside its
+    // elementwise chain (they depend only on C^ and the Khatri-Rao operand),
+    // so a wave always has independent MFMA work to issue while its VALU
+    // chain waits on latencies.  Slices tt (W), tt+1 (L) and the one being
+    // staged (tt+2) are live at once: three buffers.  Otherwise the L chain
+    // heads each t-tile and two buffers suffice.
+    constexpr bool PIPE = K5_PIPE && !PRO && RP <= 64;
+    constexpr int NB = PIPE ? 3 : 2;
+    __shared__ double sCT[NB][RP * SK];
+    __shared__ double sC[NB][16 * LDC];
     // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
     __shared__ double tsm[K5_WAVES][16 * 17];
     double* ts = tsm[wid];
@@ -360,13 +371,14 @@ void k5_fused(K5Args a) {
         double ce;
         d2v edp[2];
         double cep;
+        d4 l;  // PIPE: L of this t-tile, computed during the previous one
     };
     __shared__ double csm[K5_WAVES][96];
     double* cs = csm[wid];
     // every __shared__ array of this kernel, in bytes (160 KiB per CU; RP =
     // 256 at one wave per SIMD is the largest: ~147 KB)
     constexpr size_t LDS_BYTES =
-        sizeof(double) * (2 * RP * SK + 2 * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
+        sizeof(double) * (NB * RP * SK + NB * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
                           2 * K5_WAVES + (K5_KRLDS ? K5_WAVES * KS * 64 : 0));
     static_assert(LDS_BYTES <= 160 * 1024, "k5_fused: LDS over the 160 KiB of a CU");
     auto load = [&](int64_t tt, Regs& nx) {
@@ -396,7 +408,23 @@ void k5_fused(K5Args a) {
     };
     // one t-tile: cx holds its data; if `pf`, tile tt+1 is prefetched into nx
     // and its C^ slice staged into buffer buf^1
+    // L^T(t, ij) of the slice in sCT[b]: KS dependent MFMAs
+    auto l_mfma = [&](int b) {
+        const double* cT = sCT[b];
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        if (!(K5_EXP & 1))
+#pragma unroll
+            for (int s = 0; s < KS; ++s) acc = mfma4(cT[(4 * s + tg) * SK + il], KR(s), acc);
+        return acc;
+    };
+    // buffer after b in the rotation
+    auto bnext = [](int b) { return PIPE ? (b == NB - 1 ? 0 : b + 1) : (b ^ 1); };
+    // one t-tile; `buf` holds its C^ slice.  PIPE: bnext(buf) holds slice
+    // tt+1 (its L goes to nx.l) and slice tt+2 is staged into the buffer after
+    // that; otherwise slice tt+1 is staged into buf^1.
     auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+        const int bL = PIPE ? bnext(buf) : buf;
+        const int bS = bnext(bL);
         const int64_t tb = tm_tile_base(tile, phys(tt), ntt);
         const int64_t o = (tb >> 1) + lane;
         // prefetch first; it only needs tile tt+1's dense flag, whose slot
@@ -412,7 +440,7 @@ void k5_fused(K5Args a) {
             const bool dn1 = PRO ? false : ce_is_dense(nx.ce);
             const bool dnp1 = (PRO || !DY) ? false : ce_is_dense(nx.cep);
 #endif
-            stage_load(tt + 1);
+            stage_load(PIPE ? (tt + 2 < ntt ? tt + 2 : ntt - 1) : tt + 1);
             load(tt + 1, nx);
             // keep the prefetch ahead of the compute: the scheduler otherwise
             // sinks it next to the stores (less register pressure, no latency
@@ -455,8 +483,10 @@ void k5_fused(K5Args a) {
             }
             if (pf) load_slot(tt + 2, cx);  // cx.ce (and cx.cep) were consumed above
         }
-        const double* cT = sCT[buf];
         const double* cR = sC[buf];
+        // L of t-tile tt+1 (always computed: past the last tile it reads a
+        // slice nobody uses, into a register set nobody reads)
+        if (PIPE) nx.l = l_mfma(bL);
         double tr[4];
         if (PRO) {
 #pragma unroll
@@ -470,10 +500,14 @@ void k5_fused(K5Args a) {
             }
         } else {
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
+            if (PIPE) {
+                lacc = cx.l;
+            } else {
 #if K5_LSPLIT > 1
             // K5_LSPLIT independent accumulation chains over the K-steps, summed
             // in a fixed order (the dependent 16-MFMA chain paces one wave)
             {
+                const double* cT = sCT[buf];
                 d4 lp[K5_LSPLIT];
 #pragma unroll
                 for (int c = 0; c < K5_LSPLIT; ++c) lp[c] = d4{0.0, 0.0, 0.0, 0.0};
@@ -485,10 +519,9 @@ void k5_fused(K5Args a) {
                 for (int c = 1; c < K5_LSPLIT; ++c) lacc = lacc + lp[c];
             }
 #else
-            if (!(K5_EXP & 1))
-#pragma unroll
-                for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * SK + il], KR(s), lacc);
+            lacc = l_mfma(buf);
 #endif
+            }
             double En[4];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
@@ -580,7 +613,7 @@ void k5_fused(K5Args a) {
                 for (int m = 0; m < MT; ++m) wacc[m][0] += tr[r];
             }
         }
-        if (pf) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
+        if (pf) stage_store(bS);  // bS was last read in t-tile tt-1
         if (!(K5_EXP & 4)) __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
         // step boundary: the scheduler would otherwise hoist the next step's
         // dense-slot test (which needs this step's loads) above the barrier
@@ -601,17 +634,23 @@ void k5_fused(K5Args a) {
     if (!PRO && ce_is_dense(xa.ce)) load_dense(0, xa);
     if (!PRO && DY && ce_is_dense(xa.cep)) load_dense_p(0, xa);
     stage(0, 0);
+    if (PIPE) stage(ntt > 1 ? 1 : 0, 1);
     __syncthreads();
+    if (PIPE) xa.l = l_mfma(0);
+    xb.l = d4{0.0, 0.0, 0.0, 0.0};
     int64_t tt = 0;
+    int b = 0;  // buffer of t-tile tt's C^ slice
     for (; tt + 2 < ntt; tt += 2) {
-        body(tt, 0, xa, xb, true);
-        body(tt + 1, 1, xb, xa, true);
+        body(tt, b, xa, xb, true);
+        b = bnext(b);
+        body(tt + 1, b, xb, xa, true);
+        b = bnext(b);
     }
     if (tt + 1 < ntt) {
-        body(tt, 0, xa, xb, true);
-        body(tt + 1, 1, xb, xa, false);
+        body(tt, b, xa, xb, true);
+        body(tt + 1, bnext(b), xb, xa, false);
     } else {
-        body(tt, 0, xa, xb, false);
+        body(tt, b, xa, xb, false);
     }
     if (active) {
         // W^T C/D layout: row k = 16m + tg + 4rr, col ij = il

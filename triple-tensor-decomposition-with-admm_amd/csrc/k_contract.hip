@@ -242,6 +242,134 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
     }
 }
 
+// CP model (A^/B^ rows, not Qi's H): the same contraction with each wave
+// holding ONE ij-tile row block i0..i0+15 and walking fibres j.  Its A^ rows
+// stay in registers for the whole walk, so the Khatri-Rao operand of a step
+// is ar * B^(j,k) (4 loads + 16 multiplies), and those loads go out in the
+// same batch as the next step's T prefetch, one step ahead.  (The generic
+// kernel above loads its A^ operand after issuing the T prefetch; vmcnt is
+// in-order, so waiting on the operand also waited on the prefetch and
+// exposed the HBM latency every ij-tile.)
+// Wave = (t-block of 64 t, i-tile, part jp of the fibres); S waves per
+// t-block (padded to a multiple of 4, surplus waves contribute zeros).
+template <int RP, int LDA>
+__global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
+                                                  const double* __restrict__ Ah,
+                                                  const double* __restrict__ Bh, double* part,
+                                                  int64_t n2, int64_t n3p, int64_t ntt,
+                                                  int64_t qper, int64_t J, int S,
+                                                  const int* stop) {
+    if (*stop) return;
+    constexpr int MT = RP / 16;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int il = lane & 15, tg = lane >> 4;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t tb = wave / S;
+    const int64_t sidx = wave - tb * S;
+    const bool live = sidx < qper * J;
+    const int64_t itile = live ? sidx % qper : 0;
+    const int64_t jp = live ? sidx / qper : 0;
+    const int64_t j0 = n2 * jp / J, j1 = live ? n2 * (jp + 1) / J : j0;
+    const int64_t i0 = itile << 4;
+    const d2v* T2 = reinterpret_cast<const d2v*>(T);
+
+    // A^(i0 + 4s + tg, 16m + il) at arl[(4m + s) * 64 + lane]: in LDS, not
+    // registers (the accumulators and two prefetch sets fill the 256 VGPRs);
+    // the region is reused by the final reduction
+    double* arl = lds + wid * (MT * 4 * 64);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) arl[(4 * m + s) * 64 + lane] = Ah[(i0 + 4 * s + tg) * LDA + 16 * m + il];
+    d4 acc[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = d4{0.0, 0.0, 0.0, 0.0};
+
+    struct Nx {
+        d2v b[4][2];   // T(ij = i0 + 4s + (l>>4), t = 16(4tb+n) + (l&15)), s = 2p + q
+        double bh[MT]; // B^(j, 16m + l&15)
+    };
+    // t-tiles past the last are clamped (their columns of acc are never stored)
+    auto load = [&](int64_t j, Nx& x) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) x.bh[m] = Bh[j * LDA + 16 * m + il];
+        const int64_t g = j * qper + itile;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int64_t tt = tb * 4 + n < ntt ? tb * 4 + n : ntt - 1;
+            const int64_t o = (tm_tile_base(g, tt, ntt) >> 1) + lane;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) x.b[n][p] = __builtin_nontemporal_load(T2 + o + 64 * p);
+        }
+    };
+    // one fibre per step: take the batch issued a step ago, issue the next
+    Nx cur, nxt;
+    if (j0 < j1) load(j0, nxt);
+    for (int64_t j = j0; j < j1; ++j) {
+        cur = nxt;
+        if (j + 1 < j1) load(j + 1, nxt);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const double a = arl[(4 * m + s) * 64 + lane] * cur.bh[m];
+#pragma unroll
+                for (int n = 0; n < 4; ++n) acc[m][n] = mfma4(a, cur.b[n][s >> 1][s & 1], acc[m][n]);
+            }
+    }
+
+    // fixed-order sum of the 4 waves: (w2,w3) -> (w0,w1), then w1 -> w0
+    constexpr int PER = MT * 16;  // doubles per lane
+    __syncthreads();  // every wave is done with its A^ rows in LDS
+    if (wid >= 2) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    lds[((wid - 2) * PER + (m * 4 + n) * 4 + rr) * 64 + lane] = acc[m][n][rr];
+    }
+    __syncthreads();
+    if (wid < 2) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    acc[m][n][rr] += lds[(wid * PER + (m * 4 + n) * 4 + rr) * 64 + lane];
+    }
+    __syncthreads();
+    if (wid == 1) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) lds[((m * 4 + n) * 4 + rr) * 64 + lane] = acc[m][n][rr];
+    }
+    __syncthreads();
+    if (wid == 0) {
+        double* out = part + (int64_t)(sidx >> 2) * n3p * LDA;  // slabs of n3p x LDA
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const double v = acc[m][n][rr] + lds[((m * 4 + n) * 4 + rr) * 64 + lane];
+                    const int64_t t = tb * 64 + 16 * n + il;
+                    const int k = 16 * m + tg + 4 * rr;
+                    if (t < n3p) out[t * LDA + k] = v;
+                }
+    }
+}
+
 // M3[t][k] = sum_y part[y][t][k]  (fixed order); 4 slices per output summed in LDS
 __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ part, double* M3,
                                                    int64_t count, int nparts, const int* stop) {
@@ -257,26 +385,58 @@ __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ pa
     if (q == 0 && e < count) M3[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-// waves per t-block (multiple of 4): about two waves per SIMD in total
-int m3_split(const Geom& g) {
-    const int64_t ntb = cdiv(g.ntt, 4);
-    static const int64_t waves = [] {  // total waves (TRITD_M3_WAVES: experiments)
+// total waves of one K2 launch (TRITD_M3_WAVES: experiments): about two per SIMD
+static int64_t m3_waves() {
+    static const int64_t waves = [] {
         const char* e = std::getenv("TRITD_M3_WAVES");
         return e ? (int64_t)std::atoll(e) : (int64_t)2048;
     }();
-    int64_t S = waves / ntb;
+    return waves;
+}
+
+// generic kernel: waves per t-block (multiple of 4)
+int m3_split(const Geom& g) {
+    const int64_t ntb = cdiv(g.ntt, 4);
+    int64_t S = m3_waves() / ntb;
     if (S > g.tiles) S = g.tiles;
     S = (S + 3) / 4 * 4;
     if (S < 4) S = 4;
     return (int)S;
 }
 
-int m3_parts(const Geom& g) { return m3_split(g) / 4; }
+// CP kernel: J fibre parts per i-tile, S = qper*J waves per t-block padded to 4
+struct M3Cp {
+    int64_t qper, J;
+    int S;
+};
+static M3Cp m3_cp_split(const Geom& g) {
+    M3Cp c;
+    c.qper = g.n1p >> 4;
+    const int64_t ntb = cdiv(g.ntt, 4);
+    int64_t J = m3_waves() / (ntb * c.qper);
+    if (J < 1) J = 1;
+    if (J > g.n2) J = g.n2;
+    c.J = J;
+    c.S = (int)((c.qper * J + 3) / 4 * 4);
+    return c;
+}
+
+static bool m3_use_cp(int64_t ahj) {
+    static const bool old = std::getenv("TRITD_M3_OLD") != nullptr;  // A/B experiments
+    return ahj == 0 && !old;
+}
+
+int m3_parts(const Geom& g) {
+    const int a = m3_split(g) / 4, b = m3_cp_split(g).S / 4;
+    return a > b ? a : b;
+}
 
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
                double* M3, const int* stop, hipStream_t st, int64_t ahj, int64_t bhj) {
     if (bhj < 0) bhj = g.RP;
-    const int S = m3_split(g);
+    const bool cp = m3_use_cp(ahj);
+    const M3Cp cs = m3_cp_split(g);
+    const int S = cp ? cs.S : m3_split(g);
     const int64_t ntb = cdiv(g.ntt, 4);
     const dim3 grid((unsigned)(ntb * S / 4));
     // RP <= 64 in one pass; RP = 128 / 256 (fp64 r = 9..16) as 64-column
@@ -291,8 +451,19 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
             attr_set = true;                                                                  \
         }                                                                                     \
-        hipLaunchKernelGGL((k_m3<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF),       \
-                           Bh + (KOFF), part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj); \
+        if (cp) {                                                                             \
+            static bool attr_cp = false;                                                      \
+            if (!attr_cp) {                                                                   \
+                TRITD_HIP(hipFuncSetAttribute((const void*)k_m3_cp<RPV, LDAV>,                \
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+                attr_cp = true;                                                               \
+            }                                                                                 \
+            hipLaunchKernelGGL((k_m3_cp<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF), \
+                               Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, cs.J, S, stop); \
+        } else {                                                                              \
+            hipLaunchKernelGGL((k_m3<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF),   \
+                               Bh + (KOFF), part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj); \
+        }                                                                                     \
     }
     switch (g.RP) {
         case 16: M3_CASE(16, 16, 0) break;
@@ -312,7 +483,7 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
     TRITD_CHECK_LAUNCH();
     const int64_t count = g.n3p * g.RP;
     hipLaunchKernelGGL(k_m3_reduce, dim3((unsigned)cdiv(count, 64)), dim3(256), 0, st, part, M3,
-                       count, m3_parts(g), stop);
+                       count, S / 4, stop);
     TRITD_CHECK_LAUNCH();
 }
 
