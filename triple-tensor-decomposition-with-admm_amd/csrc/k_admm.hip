@@ -78,8 +78,11 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_EXP
 #define K5_EXP 0  // timing experiments only (tools/): drop parts of the t-tile work
 #endif
+#ifndef K5_FUSE
+#define K5_FUSE 1  // fused multiply-adds in the elementwise chain (see the t-tile body)
+#endif
 #ifndef K5_PIPE
-#define K5_PIPE 1  // L of t-tile tt+1 computed during t-tile tt (triple-buffered C^ slices)
+#define K5_PIPE 0  // L of t-tile tt+1 computed during t-tile tt (triple-buffered C^ slices)
 #endif
 
 __device__ __forceinline__ double matlab_sign(double x) {
@@ -530,9 +533,32 @@ void k5_fused(K5Args a) {
                 for (int q = 0; q < 2; ++q) {
                     const int r = 2 * p + q;
                     const double d = cx.x[0][p][q], yl = cx.x[1][p][q], e = ev[r];
+                    const double L = lacc[r];
+#if K5_FUSE
+                    // The statements of :41-53 with their multiply-adds fused
+                    // and O formed as (R1 + R2)/2 (muL == muO, :16-17,56-57, so
+                    // (muL R1 + muO R2)/(muL + muO) is exactly that average);
+                    // 18 f64 operations per element instead of 27 (K5 is
+                    // bound by the f64 pipe its MFMAs share).
+                    // Values agree with the separate-operator forms to
+                    // rounding (the parity tolerances of DESIGN.md §2).
+                    const double dL = d - L;
+                    const double yo = DY ? fma(-sc.muO_prev, e - evp[r], yl) : cx.x[2][p][q];
+                    const double R1 = fma(sc.invL, yl, dL);                 // :41
+                    const double R2 = fma(-sc.invO, yo, e);                 // :42
+                    const double On = (R1 + R2) * 0.5;                      // :43
+                    const double R3 = fma(sc.invO, yo, On);                 // :46
+                    const double Ev = R3 - fmin(fmax(R3, -sc.thr), sc.thr); // :47
+                    const double rL = dL - On;                              // :50
+                    const double rO = On - Ev;                              // :51
+                    const double YLn = fma(sc.muL, rL, yl);                 // :52
+                    const double YOn = fma(sc.muO, rO, yo);                 // :53
+                    const double Tn = fma(sc.invL_next, YLn, d - On);       // :33 (k+1)
+                    ssL = fma(rL, rL, ssL);
+                    ssO = fma(rO, rO, ssO);
+#else
                     // DY: Y_O^(k) = Y_L^(k) - muO_k (E^(k) - E^(k-1))  (header)
                     const double yo = DY ? yl - sc.muO_prev * (e - evp[r]) : cx.x[2][p][q];
-                    const double L = lacc[r];
                     const double R1 = (d - L) + sc.invL * yl;               // :41
                     const double R2 = e - sc.invO * yo;                     // :42
 #if K5_FASTDIV
@@ -575,6 +601,7 @@ void k5_fused(K5Args a) {
                     ssL += rL * rL;
                     ssO += rO * rO;
 #endif
+#endif  // K5_FUSE
                     En[r] = Ev;
                     YLn2[q] = YLn;
                     YOn2[q] = YOn;
