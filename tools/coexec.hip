@@ -32,11 +32,28 @@ __device__ double work(int iters, double seed) {
             for (int q = 0; q < 8; ++q) x[q] = __builtin_fma(x[q], 0.999999, 1e-7);
         for (int q = 0; q < 8; ++q) out += x[q];
     } else if (ROLE == 3) {
+        // 32-bit integer adds, 8 independent chains (asm: no strength reduction)
         unsigned x[8];
         for (int q = 0; q < 8; ++q) x[q] = (unsigned)(seed * 1000) + q;
         for (int i = 0; i < iters * 8; ++i)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) x[q] = (x[q] + 0x9e3779b9u) ^ (unsigned)q;
+            for (int q = 0; q < 8; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[q]) : "v"(x[(q + 1) & 7]));
+        for (int q = 0; q < 8; ++q) out += x[q];
+    } else if (ROLE == 5) {
+        // v_mov_b64 (64-bit moves), 8 chains
+        double x[8];
+        for (int q = 0; q < 8; ++q) x[q] = seed + q;
+        for (int i = 0; i < iters * 8; ++i)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) asm volatile("v_mov_b64 %0, %1" : "=v"(x[q]) : "v"(x[(q + 3) & 7]));
+        for (int q = 0; q < 8; ++q) out += x[q];
+    } else if (ROLE == 6) {
+        // v_cndmask_b32 (the compact-E selects), 8 chains
+        unsigned x[8];
+        for (int q = 0; q < 8; ++q) x[q] = (unsigned)(seed * 1000) + q;
+        for (int i = 0; i < iters * 8; ++i)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[q]) : "v"(x[(q + 1) & 7]));
         for (int q = 0; q < 8; ++q) out += x[q];
     } else if (ROLE == 4) {
         float x[8];
@@ -82,5 +99,10 @@ int main() {
     run(k_co<1, 4>, "mfma | fma_f32");
     run(k_co<2, 2>, "fma_f64 | fma_f64");
     run(k_co<1, 1>, "mfma | mfma");
+    run(k_co<0, 5>, "idle | mov_b64");
+    run(k_co<1, 5>, "mfma | mov_b64");
+    run(k_co<0, 6>, "idle | cndmask");
+    run(k_co<1, 6>, "mfma | cndmask");
+    run(k_co<3, 3>, "int | int");
     return 0;
 }

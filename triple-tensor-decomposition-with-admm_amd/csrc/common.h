@@ -105,12 +105,15 @@ struct IterScalars {
 //   words 0..3: bit masks; bit l of word w <=> the element lane l holds as
 //               MFMA C/D register element (p, q) = (w >> 1, w & 1), i.e. the
 //               TM in-tile position 128 p + 2 l + q, is nonzero
-//   words 4..31: the nonzero values, ordered by (w, l)
+//   words 4..30: the nonzero values, ordered by (w, l); unused words are +0,
+//               and word 31 always is (the decoders point lanes whose element
+//               is zero at it instead of selecting afterwards)
 // A tile with more than CE_CAP nonzeros is stored densely in E (TM) and its
 // slot masks are all ones.  Zeros are stored as +0 (MATLAB's E may hold -0,
 // which is numerically identical in every later use).
 constexpr int CE_SLOT = 32;
-constexpr int CE_CAP = CE_SLOT - 4;
+constexpr int CE_CAP = CE_SLOT - 5;
+constexpr int CE_ZERO = CE_SLOT - 1;  // the always-zero word
 
 __host__ __device__ inline int64_t tm_tile_base(int64_t g, int64_t tt, int64_t ntt) {
     return ((((g >> 2) * ntt + tt) << 2) + (g & 3)) << 8;

@@ -168,16 +168,22 @@ __device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
 __device__ __forceinline__ bool ce_decode_m(double sv, int lane, const uint64_t (&m)[4],
                                             double (&e)[4]) {
     const int svlo = __double2loint(sv), svhi = __double2hiint(sv);
+    const bool dense = m[0] == ~0ull;  // ce_is_dense
     int pre = 4;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        const int src = (pre + lanes_below(m[w])) & 63;
+        // a lane whose element is zero (and every lane of a dense tile, whose
+        // values come from E) reads the slot's always-zero word: one select
+        // on the source lane instead of two on the value; a stored tile's
+        // sources stay below CE_ZERO, so no wrap either
+        const uint64_t mw = dense ? 0ull : m[w];  // wave-uniform (SALU)
+        const int src = lane_bit(mw, lane) ? pre + lanes_below(mw) : CE_ZERO;
         const int vlo = __builtin_amdgcn_ds_bpermute(src << 2, svlo);
         const int vhi = __builtin_amdgcn_ds_bpermute(src << 2, svhi);
-        e[w] = lane_bit(m[w], lane) ? __hiloint2double(vhi, vlo) : 0.0;
-        pre += __builtin_popcountll(m[w]);
+        e[w] = __hiloint2double(vhi, vlo);
+        pre += __builtin_popcountll(mw);
     }
-    return m[0] == ~0ull;  // ce_is_dense
+    return dense;
 }
 // Store this lane's 4 elements of E (register order) as the tile's slot at
 // CE + sb, or densely into E2 at d2v offset o when they do not fit.  cs: the
@@ -466,10 +472,13 @@ void k5_fused(K5Args a) {
 #else
             const bool dn = ce_decode(cx.ce, lane, ev);
 #endif
-            ev[0] = dn ? cx.ed[0][0] : ev[0];
-            ev[1] = dn ? cx.ed[0][1] : ev[1];
-            ev[2] = dn ? cx.ed[1][0] : ev[2];
-            ev[3] = dn ? cx.ed[1][1] : ev[3];
+            if (dn) {  // wave-uniform and rare: a scalar branch, not 8 selects
+                asm volatile("" ::: "memory");  // keeps it a branch (no if-conversion)
+                ev[0] = cx.ed[0][0];
+                ev[1] = cx.ed[0][1];
+                ev[2] = cx.ed[1][0];
+                ev[3] = cx.ed[1][1];
+            }
             if (DY) {
 #if K5_SMASK
                 uint64_t mp[4];
@@ -479,10 +488,13 @@ void k5_fused(K5Args a) {
 #else
                 const bool dp = ce_decode(cx.cep, lane, evp);
 #endif
-                evp[0] = dp ? cx.edp[0][0] : evp[0];
-                evp[1] = dp ? cx.edp[0][1] : evp[1];
-                evp[2] = dp ? cx.edp[1][0] : evp[2];
-                evp[3] = dp ? cx.edp[1][1] : evp[3];
+                if (dp) {
+                    asm volatile("" ::: "memory");
+                    evp[0] = cx.edp[0][0];
+                    evp[1] = cx.edp[0][1];
+                    evp[2] = cx.edp[1][0];
+                    evp[3] = cx.edp[1][1];
+                }
             }
             if (pf) load_slot(tt + 2, cx);  // cx.ce (and cx.cep) were consumed above
         }

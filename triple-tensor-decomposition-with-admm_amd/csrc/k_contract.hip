@@ -306,21 +306,39 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
             for (int p = 0; p < 2; ++p) x.b[n][p] = __builtin_nontemporal_load(T2 + o + 64 * p);
         }
     };
+    auto mm = [&](const Nx& c) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const double a = arl[(4 * m + s) * 64 + lane] * c.bh[m];
+#pragma unroll
+                for (int n = 0; n < 4; ++n) acc[m][n] = mfma4(a, c.b[n][s >> 1][s & 1], acc[m][n]);
+            }
+    };
+#if K2_UNROLL2
+    // two register sets by name: each step computes on the batch issued a
+    // step ago while the next batch lands in the other set
+    Nx xa, xb;
+    if (j0 < j1) load(j0, xa);
+    int64_t j = j0;
+    for (; j + 1 < j1; j += 2) {
+        load(j + 1, xb);
+        mm(xa);
+        if (j + 2 < j1) load(j + 2, xa);
+        mm(xb);
+    }
+    if (j < j1) mm(xa);
+#else
     // one fibre per step: take the batch issued a step ago, issue the next
     Nx cur, nxt;
     if (j0 < j1) load(j0, nxt);
     for (int64_t j = j0; j < j1; ++j) {
         cur = nxt;
         if (j + 1 < j1) load(j + 1, nxt);
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const double a = arl[(4 * m + s) * 64 + lane] * cur.bh[m];
-#pragma unroll
-                for (int n = 0; n < 4; ++n) acc[m][n] = mfma4(a, cur.b[n][s >> 1][s & 1], acc[m][n]);
-            }
+        mm(cur);
     }
+#endif
 
     // fixed-order sum of the 4 waves: (w2,w3) -> (w0,w1), then w1 -> w0
     constexpr int PER = MT * 16;  // doubles per lane
