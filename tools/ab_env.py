@@ -9,16 +9,20 @@ from tritd import synth
 var, vals, reps = sys.argv[1], sys.argv[2].split(","), int(sys.argv[3])
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 n, r = 512, 8
-rng = np.random.default_rng(0)
-D = np.asfortranarray(rng.standard_normal((n, n, n)))
-A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
+if os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere
+    rng = np.random.default_rng(0)
+    D = np.asfortranarray(rng.standard_normal((n, n, n)))
+    A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
+else:  # the bench workload (low rank + 5 % outliers)
+    dd = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
+    D, A0, B0, C0 = dd["D"], dd["A0"], dd["B0"], dd["C0"]
 opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
 res = {v: [] for v in vals}
 for rep in range(reps):
     for v in vals:
         os.environ[var] = v
         s = tritd.Session(r, opts, A0, B0, C0, n1=n, n2=n, n3=n, D=D, device=0)
-        s.run(2); s.sync(); s.set_timing(True); s.run(iters); s.sync()
+        s.run(15); s.sync(); s.set_timing(True); s.run(iters); s.sync()
         km = s.kernel_ms()
         res[v].append((km["iteration"], km["fused_update"], km["mode3"]))
         print("%s=%s rep %d: it %.3f k5 %.3f m3 %.3f" % (var, v, rep, km["iteration"], km["fused_update"], km["mode3"]), flush=True)

@@ -21,6 +21,22 @@ __global__ void k_dep(double* sink, int iters) {
     if (s == 1.2345) sink[0] = s;
 }
 
+// v_mfma_f64_4x4x4_4b_f64 (16 blocks of... 4 blocks of 4x4x4): 512 flops each
+template <int NACC>
+__global__ void k_dep4(double* sink, int iters) {
+    double c[NACC];
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) c[q] = 0.0;
+    const double a = threadIdx.x * 1e-3, b = blockIdx.x * 1e-3 + 1.0;
+    for (int i = 0; i < iters; ++i)
+#pragma unroll
+        for (int q = 0; q < NACC; ++q) c[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c[q], 0, 0, 0);
+    double s = 0;
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) s += c[q];
+    if (s == 1.2345) sink[0] = s;
+}
+
 int main() {
     double* sink; CK(hipMalloc(&sink, 64));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -38,6 +54,9 @@ int main() {
                best * 1e6 / (total * wps));
         return 0;
     };
+    for (int t : {256, 512}) {
+        run(k_dep4<1>, 1, t); run(k_dep4<4>, 4, t); run(k_dep4<8>, 8, t);
+    }
     for (int t : {256, 512, 1024}) {
         run(k_dep<1>, 1, t); run(k_dep<2>, 2, t); run(k_dep<4>, 4, t); run(k_dep<8>, 8, t); run(k_dep<16>, 16, t);
     }

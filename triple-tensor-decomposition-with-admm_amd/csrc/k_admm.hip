@@ -81,6 +81,9 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_FUSE
 #define K5_FUSE 1  // fused multiply-adds in the elementwise chain (see the t-tile body)
 #endif
+#ifndef K5_DNBR
+#define K5_DNBR 0  // dense-tile override of the decoded E as a branch (1) or selects (0)
+#endif
 #ifndef K5_PIPE
 #define K5_PIPE 0  // L of t-tile tt+1 computed during t-tile tt (triple-buffered C^ slices)
 #endif
@@ -472,6 +475,7 @@ void k5_fused(K5Args a) {
 #else
             const bool dn = ce_decode(cx.ce, lane, ev);
 #endif
+#if K5_DNBR
             if (dn) {  // wave-uniform and rare: a scalar branch, not 8 selects
                 asm volatile("" ::: "memory");  // keeps it a branch (no if-conversion)
                 ev[0] = cx.ed[0][0];
@@ -479,6 +483,14 @@ void k5_fused(K5Args a) {
                 ev[2] = cx.ed[1][0];
                 ev[3] = cx.ed[1][1];
             }
+#else
+            // (selects, not a branch: a branch would cut the basic block and
+            // keep the scheduler from interleaving the decode with the L MFMAs)
+            ev[0] = dn ? cx.ed[0][0] : ev[0];
+            ev[1] = dn ? cx.ed[0][1] : ev[1];
+            ev[2] = dn ? cx.ed[1][0] : ev[2];
+            ev[3] = dn ? cx.ed[1][1] : ev[3];
+#endif
             if (DY) {
 #if K5_SMASK
                 uint64_t mp[4];
@@ -488,6 +500,7 @@ void k5_fused(K5Args a) {
 #else
                 const bool dp = ce_decode(cx.cep, lane, evp);
 #endif
+#if K5_DNBR
                 if (dp) {
                     asm volatile("" ::: "memory");
                     evp[0] = cx.edp[0][0];
@@ -495,6 +508,12 @@ void k5_fused(K5Args a) {
                     evp[2] = cx.edp[1][0];
                     evp[3] = cx.edp[1][1];
                 }
+#else
+                evp[0] = dp ? cx.edp[0][0] : evp[0];
+                evp[1] = dp ? cx.edp[0][1] : evp[1];
+                evp[2] = dp ? cx.edp[1][0] : evp[2];
+                evp[3] = dp ? cx.edp[1][1] : evp[3];
+#endif
             }
             if (pf) load_slot(tt + 2, cx);  // cx.ce (and cx.cep) were consumed above
         }
@@ -652,6 +671,19 @@ void k5_fused(K5Args a) {
                 for (int m = 0; m < MT; ++m) wacc[m][0] += tr[r];
             }
         }
+#if K5_EXP & 48
+        {   // timing experiment: extra VALU per t-tile (16: 32 int adds, 32: 16 f64 adds)
+            unsigned du = (unsigned)lane;
+            double dd = (double)lane;
+            if (K5_EXP & 16)
+#pragma unroll
+                for (int q = 0; q < 32; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(du) : "v"(il));
+            if (K5_EXP & 32)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) asm volatile("v_add_f64 %0, %0, %1" : "+v"(dd) : "v"(dd));
+            if (du == 12345u && dd == 1.5) ssL += 1.0;
+        }
+#endif
         if (pf) stage_store(bS);  // bS was last read in t-tile tt-1
         if (!(K5_EXP & 4)) __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
         // step boundary: the scheduler would otherwise hoist the next step's

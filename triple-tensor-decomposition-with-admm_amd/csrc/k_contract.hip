@@ -69,10 +69,70 @@ __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__
     }
 }
 
+// The same with 16-byte loads: a lane sums rows 2l, 2l+1 of a 128-row block
+// (8 independent d2v chains), the JS waves split j.
+template <int JS>
+__global__ __launch_bounds__(64 * JS) void k_m1v(const double* __restrict__ Wk,
+                                                 const double* __restrict__ Bh, double* M1,
+                                                 int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                                 const int* stop) {
+    if (*stop) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 128 + 2 * lane;
+    const int k = blockIdx.y;
+    d2v acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = d2v{0.0, 0.0};
+    if (i < n1p) {
+        const d2v* wp = reinterpret_cast<const d2v*>(Wk + (int64_t)k * plane + i);
+        const double* bp = Bh + k;
+        const int64_t ld = n1p >> 1;  // d2v per fibre
+        int64_t j = w;
+        for (; j + 7 * JS < n2; j += 8 * JS) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const d2v x = wp[(j + JS * u) * ld];
+                const double b = bp[(j + JS * u) * RP];
+                acc[u][0] = fma(x[0], b, acc[u][0]);
+                acc[u][1] = fma(x[1], b, acc[u][1]);
+            }
+        }
+        for (; j < n2; j += JS) {
+            const d2v x = wp[j * ld];
+            const double b = bp[j * RP];
+            acc[0][0] = fma(x[0], b, acc[0][0]);
+            acc[0][1] = fma(x[1], b, acc[0][1]);
+        }
+    }
+    __shared__ d2v red[JS][64];
+    red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (w == 0 && i < n1p) {
+        d2v t = red[0][lane];
+#pragma unroll
+        for (int q = 1; q < JS; ++q) t += red[q][lane];
+        M1[i * RP + k] = t[0];
+        M1[(i + 1) * RP + k] = t[1];
+    }
+}
+
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
                hipStream_t st) {
     // 4 slices when the row blocks alone fill the chip (512 rows: 36 vs 39 us
     // with 16), 16 for short shards (64 rows: 64 blocks)
+    const char* v = std::getenv("TRITD_M1V");  // experiment knob
+    const int mv = v ? std::atoi(v) : 0;
+    if (mv) {
+        const dim3 gv((unsigned)cdiv(g.n1p, 128), g.RP);
+        if (mv == 8)
+            hipLaunchKernelGGL(k_m1v<8>, gv, dim3(64 * 8), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
+        else if (mv == 16)
+            hipLaunchKernelGGL(k_m1v<16>, gv, dim3(64 * 16), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
+        else
+            hipLaunchKernelGGL(k_m1v<4>, gv, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     const dim3 grid((unsigned)cdiv(g.n1p, 64), g.RP);
     if (g.n1p >= 256)  // (two rows per lane with 16-B loads halves the waves: 72 vs 36 us)
         hipLaunchKernelGGL(k_m1<4>, grid, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
@@ -258,8 +318,13 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
                                                   const double* __restrict__ Bh, double* part,
                                                   int64_t n2, int64_t n3p, int64_t ntt,
                                                   int64_t qper, int64_t J, int S,
-                                                  const int* stop) {
+                                                  const int* stop, int stagger) {
     if (*stop) return;
+    // the second workgroup a CU receives starts later, so that the two waves
+    // sharing each SIMD are out of phase (their copy/wait boundaries would
+    // otherwise leave the matrix pipe idle together)
+    if (stagger && blockIdx.x >= 256)
+        for (int q = 0; q < stagger; ++q) __builtin_amdgcn_s_sleep(64);
     constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = threadIdx.x & 63;
@@ -439,6 +504,11 @@ static M3Cp m3_cp_split(const Geom& g) {
     return c;
 }
 
+static int m3_stagger() {  // experiment knob: TRITD_M3_STAGGER x 64 x 64 cycles
+    const char* e = std::getenv("TRITD_M3_STAGGER");
+    return e ? std::atoi(e) : 0;
+}
+
 static bool m3_use_cp(int64_t ahj) {
     static const bool old = std::getenv("TRITD_M3_OLD") != nullptr;  // A/B experiments
     return ahj == 0 && !old;
@@ -477,7 +547,7 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
                 attr_cp = true;                                                               \
             }                                                                                 \
             hipLaunchKernelGGL((k_m3_cp<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF), \
-                               Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, cs.J, S, stop); \
+                               Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, cs.J, S, stop, m3_stagger()); \
         } else {                                                                              \
             hipLaunchKernelGGL((k_m3<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF),   \
                                Bh + (KOFF), part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj); \

@@ -96,6 +96,8 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         dy_ = !f32_ && !(dy && std::atoi(dy) == 0);
         const char* gm = std::getenv("TRITD_GRAM_MAIN");      // overlapped (1-GPU) schedule
         gram_main_ = gm ? std::atoi(gm) : 0;
+        const char* sbm = std::getenv("TRITD_SB_MAIN");
+        sb_main_ = !(sbm && std::atoi(sbm) == 0);
         const char* gms = std::getenv("TRITD_GRAM_MAIN_SH");  // sharded schedule
         gram_main_sh_ = gms ? std::atoi(gms) : 0;
         const char* sh = std::getenv("TRITD_SHOV");
@@ -590,14 +592,24 @@ void Session::iterate_overlapped(int k) {
     do_m1();
     TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
     do_apply_A(GinvA_.p);
-    if (gsel(0) == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
-    TRITD_HIP(hipEventRecord(evAtA_, st_));
-    TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
-    if (gsel(0) == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
-    solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, side_);
-    TRITD_HIP(hipEventRecord(evSB_, side_));
-    do_m2(M2);
-    TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
+    if (sb_main_ && gs == side_) {
+        // Gram A^TA and solve B are on the critical path (M2 beside them is
+        // only ~20 us): on the main stream they cost their own time, on the
+        // side stream they cost that plus two cross-stream waits (each event
+        // wait or record widens a kernel boundary by ~6 us, measured)
+        launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+        do_m2(M2);
+    } else {
+        if (gsel(0) == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+        TRITD_HIP(hipEventRecord(evAtA_, st_));
+        TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
+        if (gsel(0) == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, side_);
+        TRITD_HIP(hipEventRecord(evSB_, side_));
+        do_m2(M2);
+        TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
+    }
     do_apply_B(M2, GinvB_.p);
     if (gsel(1) == st_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));

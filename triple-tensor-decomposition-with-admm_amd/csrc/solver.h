@@ -106,6 +106,7 @@ class Session {
     bool overlap_ = false;
     int ovmode_ = 2;
     int gram_main_ = 0, gram_main_sh_ = 0;  // Grams on the main stream (bit 0 A, 1 B, 2 C)
+    bool sb_main_ = true;  // 1-GPU schedule: Gram A^TA and solve B on the main stream
     int rot_ = 1;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
