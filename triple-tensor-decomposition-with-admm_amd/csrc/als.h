@@ -78,7 +78,7 @@ class AlsSession {
     int k_enq_ = 0;
     bool quiet_ = false;
     DBuf X_, XT_, Wk_;  // X tile-major, X in TX order (K2), W = X x3 C^
-    DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
+    DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, GinvA_, GinvB_, GinvC_, BtB_, CtC_;
     DBuf red0_, red1_, red2_, fitpart_, m3part_, sqpart_, errHist_;
     uint32_t flags_ = 0;
     int* ctrl_ = nullptr;  // [0] stop, [1] errHist entries, [2] pinv-tolerance flag

@@ -87,6 +87,9 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_PIPE
 #define K5_PIPE 0  // L of t-tile tt+1 computed during t-tile tt (triple-buffered C^ slices)
 #endif
+#ifndef K5_WPE
+#define K5_WPE 2  // waves per SIMD at RP <= 64 (one wave: 1.243 vs 0.998 ms, round 3)
+#endif
 
 __device__ __forceinline__ double matlab_sign(double x) {
     // sign(): 1 / -1 / 0 (also for -0), NaN stays NaN; selects only, no
@@ -243,7 +246,7 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
 // Two waves per SIMD (VGPRs + AGPRs <= 256): at one wave per SIMD the
 // streams do not keep enough bytes in flight (measured +6 % K5 time).
 template <int RP, bool PRO, bool DY>
-__global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(RP >= 128 ? 1 : 2, 2)))
+__global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(RP >= 128 ? 1 : K5_WPE, K5_WPE)))
 void k5_fused(K5Args a) {
     if (*a.stop) return;
     constexpr int KS = RP / 4;   // MFMA K-steps for L

@@ -661,10 +661,10 @@ constexpr int SOLVE_ROWS = SOLVE_ROWS_OVERRIDE;  // tools/solve_bench.hip
 // local row) into buffer P&1 by the previous step.  All reads are issued
 // first; the row of pivot P+1 is updated before the others and published
 // into the other buffer at once, so the barrier only waits on that.
-template <int RP, int P>
-__device__ __forceinline__ void sweep_step(double (&a)[SOLVE_ROWS], double* rowbuf, double* pivs,
-                                           int c, int w) {
-    constexpr int RW = SOLVE_ROWS, NW = RP / RW, W = P / RW, L = P % RW;
+template <int RP, int RW, int P>
+__device__ __forceinline__ void sweep_step(double (&a)[RW], double* rowbuf, double* pivs, int c,
+                                           int w) {
+    constexpr int NW = RP / RW, W = P / RW, L = P % RW;
     const double* row = rowbuf + (P & 1) * NW * 64 + W * 64;  // a_Pc == a_cP
     const double piv = row[P];
     const double rc = row[c];
@@ -694,10 +694,10 @@ __device__ __forceinline__ void sweep_step(double (&a)[SOLVE_ROWS], double* rowb
     __syncthreads();
 }
 
-template <int RP, int... Ps>
-__device__ __forceinline__ void sweep_all(double (&a)[SOLVE_ROWS], double* rowbuf, double* pivs,
-                                          int c, int w, std::integer_sequence<int, Ps...>) {
-    (sweep_step<RP, Ps>(a, rowbuf, pivs, c, w), ...);
+template <int RP, int RW, int... Ps>
+__device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, double* pivs, int c,
+                                          int w, std::integer_sequence<int, Ps...>) {
+    (sweep_step<RP, RW, Ps>(a, rowbuf, pivs, c, w), ...);
 }
 
 template <int RP>
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __
     }
     rowbuf[w * 64 + c] = a[0];  // row 0 (wave 0's)
     __syncthreads();
-    sweep_all<RP>(a, rowbuf, pivs, c, w, std::make_integer_sequence<int, RP>{});
+    sweep_all<RP, RW>(a, rowbuf, pivs, c, w, std::make_integer_sequence<int, RP>{});
     // out through LDS, then a linear copy that zeroes the pad (the sweep
     // leaves the identity-pad block and the zero blocks beside it untouched)
 #pragma unroll
@@ -748,6 +748,188 @@ __global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Ginv = inv(P o Q + alpha I) for RP <= 64 by Newton-Schulz refinement of the
+// previous inverse of the same Gram slot (the output buffer's contents on
+// entry), with the symmetric Gauss-Jordan sweep above as the fallback.
+//
+// The Grams of consecutive ADMM iterations differ little once the factors
+// settle, so X0 = the last inverse is already close: E = I - G X0 is small
+// and X <- X + X E squares it per step (E' = E^2).  Every step is two RP^3
+// GEMMs on v_mfma_f64_16x16x4_f64 (one 16x16 tile per wave, operands in
+// LDS) and one fixed-order norm, ~0.5 us each, against the sweep's RP
+// dependent pivot steps of ~0.3 us.  The loop stops once the update is
+// below the rounding floor: after an update whose ||E||_F < 1e-7 (the new
+// error is ~||E||^2 < 1e-14), or as soon as ||E|| stops halving (cond(G) *
+// eps reached; the last X is kept).  With ||E0||_F >= 1/2 (early iterations,
+// a zero or stale buffer, a NaN) the kernel runs the sweep instead, so the
+// result is an inverse to working accuracy either way.
+//
+// pinv-tolerance flag (triple_decomp_ADMM.m:78,86,93 use pinv): the sweep
+// path compares its LDL^T pivots as k_solve does; the Newton path uses the
+// bounds sigma_min >= 1/||X||_F and sigma_max <= ||G||_F, i.e. it raises
+// the flag whenever the sweep could (and up to sqrt(R) earlier).
+//
+// Waves: RP/4 (the sweep runs 4 rows per lane); the Newton GEMMs use the
+// first (RP/16)^2 of them.
+// ---------------------------------------------------------------------------
+template <int RP>
+__global__ __launch_bounds__(RP * 16) void k_solve_ns(const double* __restrict__ P,
+                                                     const double* __restrict__ Q, int R,
+                                                     double alpha, double* Ginv, int* flags,
+                                                     const int* stop) {
+    if (*stop) return;
+    __builtin_amdgcn_s_setprio(3);  // beside K2 / K5 on the side stream: win issue
+    constexpr int NWV = RP / 4, NT = RP / 16, LD = RP + 1, KS = RP / 4, RW = 4;
+    constexpr int NTH = 64 * NWV;
+    __shared__ double Gs[RP * LD], Xs[RP * LD], Es[RP * LD];
+    __shared__ double rowbuf[2 * NWV * 64];
+    __shared__ double pivs[RP];
+    __shared__ double red[2][NWV];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m = lane & 15, kq = lane >> 4;
+    const bool tw = w < NT * NT;  // this wave owns a 16 x 16 tile of the GEMMs
+    const int ta = tw ? w / NT : 0, tb = tw ? w - (w / NT) * NT : 0;
+    double gss = 0.0;  // ||G||_F^2 partial
+    {
+        constexpr int NE = RP * RP / NTH;  // = RP/16 elements per thread
+        static_assert(RP * RP % NTH == 0, "k_solve_ns: element split");
+        double pv[NE], qv[NE], xv[NE];
+#pragma unroll
+        for (int q = 0; q < NE; ++q) {  // every load issued before the first use
+            const int e = tid + q * NTH;
+            pv[q] = P[e];
+            qv[q] = Q[e];
+            xv[q] = Ginv[e];
+        }
+#pragma unroll
+        for (int q = 0; q < NE; ++q) {
+            const int e = tid + q * NTH;
+            const int i = e / RP, c = e - (e / RP) * RP;
+            const bool in = i < R && c < R;
+            const double pq = pv[q] * qv[q];
+            const double g = in ? ((i == c) ? pq + alpha : pq) : ((i == c) ? 1.0 : 0.0);
+            Gs[i * LD + c] = g;
+            Xs[i * LD + c] = in ? xv[q] : ((i == c) ? 1.0 : 0.0);
+            if (in) gss = fma(g, g, gss);
+        }
+    }
+    auto wave_sum = [&](double v) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        return v;
+    };
+    // C = A B for this wave's tile (A, B in LDS, row stride LD)
+    auto gemm = [&](const double* A, const double* B) {
+        double a[KS], b[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            a[s] = A[(16 * ta + m) * LD + 4 * s + kq];
+            b[s] = B[(4 * s + kq) * LD + 16 * tb + m];
+        }
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = mfma4(a[s], b[s], acc);
+        return acc;
+    };
+    // C/D element r of lane l: (16 ta + (l>>4) + 4 r, 16 tb + (l&15))
+    auto at = [&](int r) { return (16 * ta + kq + 4 * r) * LD + 16 * tb + m; };
+    __syncthreads();
+    bool sweep = false;
+    double nprev = 0.0;
+    for (int it = 0;; ++it) {
+        double ss = 0.0;
+        if (tw) {
+            const d4 t = gemm(Gs, Xs);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * ta + kq + 4 * r, col = 16 * tb + m;
+                const double ev = ((row == col) ? 1.0 : 0.0) - t[r];
+                Es[at(r)] = ev;
+                ss = fma(ev, ev, ss);
+            }
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) red[0][w] = ss;
+        __syncthreads();
+        double n2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < NWV; ++q) n2 += red[0][q];  // same order in every thread
+        const double n = sqrt(n2);
+        if (it == 0 && !(n < 0.5)) {  // no usable start: sweep
+            sweep = true;
+            break;
+        }
+        if (it > 0 && !(n < 0.5 * nprev)) break;  // rounding floor: keep X
+        if (tw) {
+            const d4 u = gemm(Xs, Es);
+            double xv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xv[r] = Xs[at(r)];
+            __syncthreads();  // every wave has read Xs, Es and red
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Xs[at(r)] = xv[r] + u[r];
+        } else {
+            __syncthreads();
+        }
+        __syncthreads();
+        nprev = n;
+        if (n < 1e-7 || it >= 7) break;  // the update left ~n^2 < 1e-14
+    }
+    double minpiv = 0.0, maxpiv = 0.0;  // sweep: LDL^T pivots; Newton: sigma bounds
+    if (sweep) {
+        // Gauss-Jordan sweep of G (k_solve with 4 rows per lane); -inv lands in Xs
+        const int c = lane, cc = c < RP ? c : 0;
+        double a[RW];
+#pragma unroll
+        for (int q = 0; q < RW; ++q) a[q] = Gs[(RW * w + q) * LD + cc];
+        rowbuf[w * 64 + c] = a[0];
+        __syncthreads();
+        sweep_all<RP, RW>(a, rowbuf, pivs, c, w, std::make_integer_sequence<int, RP>{});
+        if (c < RP)
+#pragma unroll
+            for (int q = 0; q < RW; ++q) Xs[(RW * w + q) * LD + c] = -a[q];
+        __syncthreads();
+        if (tid == 0) {
+            minpiv = 1e308;
+            for (int p = 0; p < R; ++p) {
+                minpiv = fmin(minpiv, pivs[p]);
+                maxpiv = fmax(maxpiv, pivs[p]);
+            }
+        }
+    }
+    double xss = 0.0;
+    for (int e = tid; e < RP * RP; e += NTH) {
+        const int i = e / RP, j = e - (e / RP) * RP;
+        const bool in = i < R && j < R;
+        const double x = in ? Xs[i * LD + j] : 0.0;
+        Ginv[e] = x;
+        xss = fma(x, x, xss);
+    }
+    if (!sweep) {
+        xss = wave_sum(xss);
+        gss = wave_sum(gss);
+        if (lane == 0) {
+            red[0][w] = xss;
+            red[1][w] = gss;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double x2 = 0.0, g2 = 0.0;
+            for (int q = 0; q < NWV; ++q) {
+                x2 += red[0][q];
+                g2 += red[1][q];
+            }
+            minpiv = 1.0 / sqrt(x2);
+            maxpiv = sqrt(g2);
+        }
+    }
+    if (tid == 0) {
+        const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);  // pinv: R*eps(sigma_max)
+        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Ginv = inv(P o Q + alpha I) for RP in {128, 256} (fp32 path, r = 9..16):
@@ -1065,16 +1247,17 @@ void launch_solve_blk(int R, const double* P, const double* Q, double alpha, dou
                        alpha, Ginv, flags, stop);
 }
 
-// RP <= 64: per-pivot register sweep (k_solve); RP = 128: blocked sweep
-// (k_solve_blk); RP = 256: k_solve_big.  TRITD_SOLVE=blk runs the blocked
-// sweep at RP <= 64 too (timing / accuracy experiments), =sweep keeps
-// k_solve_big at 128.
+// RP <= 64: Newton-Schulz refinement of the previous inverse with the
+// per-pivot sweep as fallback (k_solve_ns); RP = 128: blocked sweep
+// (k_solve_blk); RP = 256: k_solve_big.  TRITD_SOLVE=gj runs the plain sweep
+// (k_solve) at RP <= 64, =blk the blocked sweep there (timing / accuracy
+// experiments), =sweep keeps k_solve_big at 128.
 static int solve_mode() {
     static const int v = [] {
         const char* e = std::getenv("TRITD_SOLVE");
         if (!e) return 0;
         const std::string x(e);
-        return x == "blk" ? 1 : (x == "sweep" ? 2 : 0);
+        return x == "blk" ? 1 : (x == "sweep" ? 2 : (x == "gj" ? 3 : 0));
     }();
     return v;
 }
@@ -1093,6 +1276,23 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
             case 48: launch_solve_blk<48>(R, P, Q, alpha, Ginv, flags, stop, st); break;
             case 64: launch_solve_blk<64>(R, P, Q, alpha, Ginv, flags, stop, st); break;
             case 128: launch_solve_blk<128>(R, P, Q, alpha, Ginv, flags, stop, st); break;
+            default: throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
+        }
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
+    if (RP <= 64 && solve_mode() == 0) {
+        switch (RP) {
+#define NS_CASE(RPV)                                                                            \
+    case RPV:                                                                                   \
+        hipLaunchKernelGGL(k_solve_ns<RPV>, dim3(1), dim3(RPV * 16), 0, st, P, Q, R, alpha, Ginv, \
+                           flags, stop);                                                        \
+        break;
+            NS_CASE(16)
+            NS_CASE(32)
+            NS_CASE(48)
+            NS_CASE(64)
+#undef NS_CASE
             default: throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
         }
         TRITD_CHECK_LAUNCH();

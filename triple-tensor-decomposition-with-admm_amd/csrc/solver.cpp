@@ -163,11 +163,11 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     Ch_.alloc(g_.n3p * g_.RP);
     ChT_.alloc((size_t)g_.RP * g_.n3p);
     M1_.alloc_bytes((size_t)g_.n1p * g_.RP * es_);
-    Ginv_.alloc((size_t)g_.RP * g_.RP);
-    if (overlap_ || shov_) {
-        GinvA_.alloc((size_t)g_.RP * g_.RP);
-        GinvB_.alloc((size_t)g_.RP * g_.RP);
-        GinvC_.alloc((size_t)g_.RP * g_.RP);
+    // one inverse per Gram slot, kept across iterations: each solve refines
+    // the previous inverse of its own slot (k_solve_ns); zero = no start
+    for (DBuf* b : {&GinvA_, &GinvB_, &GinvC_}) {
+        b->alloc((size_t)g_.RP * g_.RP);
+        TRITD_HIP(hipMemsetAsync(b->p, 0, b->bytes(), st_));
     }
     BtB_.alloc((size_t)g_.RP * g_.RP);
     CtC_.alloc((size_t)g_.RP * g_.RP);
@@ -464,8 +464,8 @@ void Session::phaseA(int k) {
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
     do_m1();
-    solve(0, BtB_.p, CtC_.p, o_.lambda2, Ginv_.p, st_);
-    do_apply_A(Ginv_.p);
+    solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, st_);
+    do_apply_A(GinvA_.p);
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     do_m2(M2);
 }
@@ -475,8 +475,8 @@ void Session::phaseB(int k) {
     const int RP = g_.RP;
     const double* M2 = red1_.p;
     const double* AtA = red1_.p + g_.n2 * RP;
-    solve(1, AtA, CtC_.p, o_.lambda2, Ginv_.p, st_);
-    do_apply_B(M2, Ginv_.p);
+    solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+    do_apply_B(M2, GinvB_.p);
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     mark(1);
     do_m3();
@@ -486,8 +486,8 @@ void Session::phaseB(int k) {
 void Session::phaseC(int k) {
     const int RP = g_.RP;
     const double* AtA = red1_.p + g_.n2 * RP;
-    solve(2, AtA, BtB_.p, 1e-9, Ginv_.p, st_);  // :93 ridge
-    do_apply_C(Ginv_.p);
+    solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, st_);  // :93 ridge
+    do_apply_C(GinvC_.p);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     launch_k5_full(k, /*fused_finish=*/false);
 }

@@ -151,7 +151,7 @@ class Session {
     DBuf CE2_;
     double* ce_buf(int k) const { return (dy_ && (k & 1)) ? CE2_.p : CE_.p; }
     double* e_buf(int k) const { return (dy_ && (k & 1)) ? YO_.p : E_.p; }
-    DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, Ginv_, BtB_, CtC_;
+    DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, BtB_, CtC_;
     // Qi model (opts.model = TRITD_MODEL_QI, k_qi.hip): H = the Qi mode-3 design
     // matrix by rows ij (K2/K5 Khatri-Rao operand), an all-ones RP x RP block
     // (the Hadamard factor of the solve and the B operand of the KR product),
