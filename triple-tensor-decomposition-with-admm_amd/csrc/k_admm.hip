@@ -87,8 +87,28 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_PIPE
 #define K5_PIPE 0  // L of t-tile tt+1 computed during t-tile tt (triple-buffered C^ slices)
 #endif
+#ifndef K5_PROF
+#define K5_PROF 0  // timing experiments only: s_memtime phase profile of the t-walk (tools/k5_prof.py)
+#endif
 #ifndef K5_WPE
 #define K5_WPE 2  // waves per SIMD at RP <= 64 (one wave: 1.243 vs 0.998 ms, round 3)
+#endif
+
+#if K5_PROF
+// phase clocks of the t-walk summed over waves: [0..7] phases, [8] steps
+__device__ unsigned long long g_k5prof[16];
+#define K5_PT(n)                                          \
+    do {                                                  \
+        __builtin_amdgcn_sched_barrier(0);                \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        if ((n) > 0) pacc[(n) - 1] += t_ - plast;         \
+        plast = t_;                                       \
+        __builtin_amdgcn_sched_barrier(0);                \
+    } while (0)
+#else
+#define K5_PT(n) \
+    do {         \
+    } while (0)
 #endif
 
 __device__ __forceinline__ double matlab_sign(double x) {
@@ -437,7 +457,14 @@ void k5_fused(K5Args a) {
     // one t-tile; `buf` holds its C^ slice.  PIPE: bnext(buf) holds slice
     // tt+1 (its L goes to nx.l) and slice tt+2 is staged into the buffer after
     // that; otherwise slice tt+1 is staged into buf^1.
+#if K5_PROF
+    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, plast = 0, psteps = 0;
+#endif
     auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+        K5_PT(0);
+#if K5_PROF
+        ++psteps;
+#endif
         const int bL = PIPE ? bnext(buf) : buf;
         const int bS = bnext(bL);
         const int64_t tb = tm_tile_base(tile, phys(tt), ntt);
@@ -467,6 +494,7 @@ void k5_fused(K5Args a) {
             if (!PRO && dn1) load_dense(tt + 1, nx);
             if (!PRO && DY && dnp1) load_dense_p(tt + 1, nx);
         }
+        K5_PT(1);
         double ev[4], evp[4];
         if (!PRO) {
 #if K5_SMASK
@@ -520,6 +548,7 @@ void k5_fused(K5Args a) {
             }
             if (pf) load_slot(tt + 2, cx);  // cx.ce (and cx.cep) were consumed above
         }
+        K5_PT(2);
         const double* cR = sC[buf];
         // L of t-tile tt+1 (always computed: past the last tile it reads a
         // slice nobody uses, into a register set nobody reads)
@@ -559,6 +588,7 @@ void k5_fused(K5Args a) {
             lacc = l_mfma(buf);
 #endif
             }
+            K5_PT(3);
             double En[4];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
@@ -644,7 +674,9 @@ void k5_fused(K5Args a) {
                 st2(YLn2, YL2 + o + 64 * p);
                 if (!DY) st2(YOn2, YO2 + o + 64 * p);
             }
+            K5_PT(4);
             ce_encode(En, lane, cs, CEout, (tb >> 8) * CE_SLOT, Eout2, o, ndense);
+            K5_PT(5);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
         if (K5_EXP & 8) {
@@ -663,6 +695,7 @@ void k5_fused(K5Args a) {
             st2(tv, T2 + o + 64 * p);
         }
         }
+        K5_PT(6);
         // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -687,11 +720,13 @@ void k5_fused(K5Args a) {
             if (du == 12345u && dd == 1.5) ssL += 1.0;
         }
 #endif
+        K5_PT(7);
         if (pf) stage_store(bS);  // bS was last read in t-tile tt-1
         if (!(K5_EXP & 4)) __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
         // step boundary: the scheduler would otherwise hoist the next step's
         // dense-slot test (which needs this step's loads) above the barrier
         __builtin_amdgcn_sched_barrier(0);
+        K5_PT(8);
     };
 
     Regs xa, xb;
@@ -736,6 +771,12 @@ void k5_fused(K5Args a) {
                 a.Wk[(int64_t)(16 * m + tg + 4 * rr) * a.plane + wbase] = wacc[m][rr];
     }
 
+#if K5_PROF
+    if (!PRO && lane == 0) {
+        for (int q = 0; q < 8; ++q) atomicAdd(&g_k5prof[q], (unsigned long long)pacc[q]);
+        atomicAdd(&g_k5prof[8], (unsigned long long)psteps);
+    }
+#endif
     if (!PRO && ndense && lane == 0)  // spread over DENSE_SLOTS counters
         atomicAdd(a.dense_tiles + ((blockIdx.x * K5_WAVES + wid) & (DENSE_SLOTS - 1)),
                   (unsigned long long)ndense);
@@ -765,6 +806,19 @@ void k5_fused(K5Args a) {
 }
 
 int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }
+
+#if K5_PROF
+}  // namespace tritd
+// timing experiments only (tools/k5_prof.py): read and clear the phase clocks
+extern "C" int tritd_k5prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tritd::g_k5prof), 16 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return 1;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(tritd::g_k5prof), z, sizeof z) == hipSuccess ? 0 : 1;
+}
+namespace tritd {
+#endif
 
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st) {
     const dim3 grid(k5_grid(g)), block(64 * K5_WAVES);
