@@ -55,16 +55,40 @@ def test_rccl_single_rank_session(tritd):
                orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_single_gpu_schedules_match_golden(tritd, fused, monkeypatch):
+    """TRITD_FUSED=1 (default): one stream, solves of C and A(k+1) inside
+    K2 / K5; 0: the side-stream schedule (Session::iterate_overlapped)."""
+    import tritd_oracle as orc
+    monkeypatch.setenv("TRITD_FUSED", fused)
+    g = load_golden("g17x16x20_r8")
+    n1, n2, n3 = g["D"].shape
+    s = tritd.Session(g["r"], g["opts"], g["A0"], g["B0"], g["C0"], n1=n1, n2=n2, n3=n3,
+                      D=g["D"], device=0)
+    s.run(g["opts"]["maxIter"])
+    res = s.get()
+    s.close()
+    assert res["k"] == g["k"]
+    assert rel(res["O"], g["O"]) <= 1e-9 and rel(res["E"], g["E"]) <= 1e-9
+    assert rel(orc.triple_product(res["A"], res["B"], res["C"]),
+               orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
+    np.testing.assert_allclose(res["errHist"], g["errHist"], rtol=1e-8, atol=ATOL_ERR)
+
+
 @pytest.mark.parametrize("name", ["g30_r3", "g12x10x8_r2_stop"])
 def test_sharded_schedule_matches_phase_order(tritd, name, monkeypatch):
-    """With a communicator the Grams of B, C and the solves of C, A(k+1) run
-    on a side stream (Session::iterate_sharded); same kernels on the same
-    inputs as the phase-serial order (TRITD_SHOV=0), so bitwise equal."""
+    """With a communicator the default schedule is the single-stream one
+    (Session::iterate_fused: the solves of C and A(k+1) in an extra workgroup
+    of K2 / K5, as a Gauss-Jordan sweep), TRITD_FUSED=0 the side-stream one
+    (Session::iterate_sharded), TRITD_SHOV=0 the phase-serial order.  The
+    serial order refines solves C, A with Newton-Schulz (k_solve_ns), so the
+    schedules agree to rounding, not bitwise; each is bitwise reproducible."""
     g = load_golden(name)
     n1, n2, n3 = g["D"].shape
     out = []
-    for shov in ("1", "0"):
+    for shov, fused in (("1", "1"), ("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("TRITD_SHOV", shov)
+        monkeypatch.setenv("TRITD_FUSED", fused)
         comm = tritd.Comm(tritd.Comm.unique_id(), 1, 0, 0)
         s = tritd.Session(g["r"], g["opts"], g["A0"], g["B0"], g["C0"], n1=n1, n2=n2, n3=n3,
                           D=g["D"], device=0, comm=comm)
@@ -72,9 +96,12 @@ def test_sharded_schedule_matches_phase_order(tritd, name, monkeypatch):
         out.append(s.get())
         s.close()
         comm.close()
-    assert out[0]["k"] == out[1]["k"] == g["k"]
+    assert all(o["k"] == g["k"] for o in out)
     for key in ("A", "B", "C", "O", "E", "errHist"):
-        np.testing.assert_array_equal(out[0][key], out[1][key])
+        np.testing.assert_array_equal(out[0][key], out[1][key])  # run to run
+        for o in out[2:]:
+            np.testing.assert_allclose(o[key], out[0][key], rtol=1e-10,
+                                       atol=1e-12 * np.abs(out[0][key]).max())
 
 
 def test_config2_sensor_shape_vs_c_oracle(tritd, cref):

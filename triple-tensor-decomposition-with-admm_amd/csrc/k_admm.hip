@@ -41,6 +41,7 @@
 // Elementwise arithmetic follows MATLAB's expression order exactly; the file
 // is compiled with -ffp-contract=off so no statement is fused into an FMA.
 #include "kernels.h"
+#include "sweep.h"
 
 namespace tritd {
 
@@ -269,6 +270,18 @@ template <int RP, bool PRO, bool DY>
 __global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(RP >= 128 ? 1 : K5_WPE, K5_WPE)))
 void k5_fused(K5Args a) {
     if (*a.stop) return;
+    // side job: workgroup 0 runs the R x R solve of the next update_A
+    // (sweep.h) beside the walk, so no second stream is needed for it
+    constexpr bool SIDE_OK = !PRO && RP <= 64;
+    const int side = SIDE_OK ? a.side.on : 0;
+    if constexpr (SIDE_OK) {
+        if (side && blockIdx.x == 0) {
+            __shared__ double srow[2 * 4 * 64 + RP];
+            side_solve<RP>(a.side, srow, srow + 2 * 4 * 64);
+            return;
+        }
+    }
+    const int64_t bid = (int64_t)blockIdx.x - side;  // this workgroup's group of ij-tiles
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
     constexpr int LDC = RP + 16; // row stride of the [t][k] C^ slice (2*LDC = 32 mod 64: no bank conflicts)
@@ -283,7 +296,7 @@ void k5_fused(K5Args a) {
     const int wid = K5_SWID ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6);
     const int il = lane & 15;
     const int tg = lane >> 4;
-    const int64_t tile = (int64_t)blockIdx.x * K5_WAVES + wid;
+    const int64_t tile = bid * K5_WAVES + wid;
     const bool active = tile < a.tiles;
     const int64_t qper = a.n1p >> 4;
     const int64_t j = active ? tile / qper : 0;
@@ -310,7 +323,7 @@ void k5_fused(K5Args a) {
     // Rotated t-walk: resident workgroups start at different t-tiles so that
     // their concurrent streams do not advance in lockstep 64 KB apart (HBM
     // channel hot-spotting).  Any fixed order is deterministic.
-    const int64_t rot = a.rot ? ((int64_t)blockIdx.x * 7) % ntt : 0;
+    const int64_t rot = a.rot ? (bid * 7) % ntt : 0;
     auto phys = [&](int64_t tt) { int64_t x = tt + rot; return x >= ntt ? x - ntt : x; };
     // Staging is split so that its global loads are issued before the tile
     // prefetch and its LDS writes come after this t-tile's compute: vmcnt is
@@ -778,7 +791,7 @@ void k5_fused(K5Args a) {
     }
 #endif
     if (!PRO && ndense && lane == 0)  // spread over DENSE_SLOTS counters
-        atomicAdd(a.dense_tiles + ((blockIdx.x * K5_WAVES + wid) & (DENSE_SLOTS - 1)),
+        atomicAdd(a.dense_tiles + ((bid * K5_WAVES + wid) & (DENSE_SLOTS - 1)),
                   (unsigned long long)ndense);
     if (!PRO) {
         // fixed-order block reduction of the residual norms
@@ -799,8 +812,8 @@ void k5_fused(K5Args a) {
                 x += red[0][w];
                 y += red[1][w];
             }
-            a.partial[2 * blockIdx.x] = x;
-            a.partial[2 * blockIdx.x + 1] = y;
+            a.partial[2 * bid] = x;
+            a.partial[2 * bid + 1] = y;
         }
     }
 }
@@ -821,7 +834,8 @@ namespace tritd {
 #endif
 
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st) {
-    const dim3 grid(k5_grid(g)), block(64 * K5_WAVES);
+    if (a.side.on && (prologue || g.RP > 64)) throw Error(TRITD_ERR_ARG, "K5 side solve: RP <= 64 only");
+    const dim3 grid(k5_grid(g) + (a.side.on ? 1 : 0)), block(64 * K5_WAVES);
 #define K5_CASE(RPV)                                                                 \
     case RPV:                                                                        \
         if (prologue)                                                                \

@@ -15,6 +15,7 @@
 #include <utility>
 
 #include "kernels.h"
+#include "sweep.h"
 
 namespace tritd {
 
@@ -318,19 +319,26 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
                                                   const double* __restrict__ Bh, double* part,
                                                   int64_t n2, int64_t n3p, int64_t ntt,
                                                   int64_t qper, int64_t J, int S,
-                                                  const int* stop, int stagger) {
+                                                  const int* stop, int stagger, SideSolve side) {
     if (*stop) return;
+    // side job: workgroup 0 runs the R x R solve of update_C (sweep.h)
+    if (side.on && blockIdx.x == 0) {
+        extern __shared__ __attribute__((aligned(16))) double slds[];
+        side_solve<RP>(side, slds, slds + 2 * 4 * 64);
+        return;
+    }
+    const int64_t bid = (int64_t)blockIdx.x - side.on;
     // the second workgroup a CU receives starts later, so that the two waves
     // sharing each SIMD are out of phase (their copy/wait boundaries would
     // otherwise leave the matrix pipe idle together)
-    if (stagger && blockIdx.x >= 256)
+    if (stagger && bid >= 256)
         for (int q = 0; q < stagger; ++q) __builtin_amdgcn_s_sleep(64);
     constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int il = lane & 15, tg = lane >> 4;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + wid;
+    const int64_t wave = bid * 4 + wid;
     const int64_t tb = wave / S;
     const int64_t sidx = wave - tb * S;
     const bool live = sidx < qper * J;
@@ -520,9 +528,11 @@ int m3_parts(const Geom& g) {
 }
 
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
-               double* M3, const int* stop, hipStream_t st, int64_t ahj, int64_t bhj) {
+               double* M3, const int* stop, hipStream_t st, int64_t ahj, int64_t bhj,
+               const SideSolve& side) {
     if (bhj < 0) bhj = g.RP;
     const bool cp = m3_use_cp(ahj);
+    if (side.on && (!cp || g.RP > 64)) throw Error(TRITD_ERR_ARG, "K2 side solve: CP kernel, RP <= 64 only");
     const M3Cp cs = m3_cp_split(g);
     const int S = cp ? cs.S : m3_split(g);
     const int64_t ntb = cdiv(g.ntt, 4);
@@ -546,8 +556,9 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
                 attr_cp = true;                                                               \
             }                                                                                 \
-            hipLaunchKernelGGL((k_m3_cp<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF), \
-                               Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, cs.J, S, stop, m3_stagger()); \
+            hipLaunchKernelGGL((k_m3_cp<RPV, LDAV>), dim3(grid.x + side.on), dim3(256), lds, st, T, \
+                               Ah + (KOFF), Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, \
+                               cs.J, S, stop, m3_stagger(), side);                   \
         } else {                                                                              \
             hipLaunchKernelGGL((k_m3<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF),   \
                                Bh + (KOFF), part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj); \
@@ -656,49 +667,6 @@ constexpr int SOLVE_ROWS = 8;  // matrix rows per lane; RP/8 waves
 #else
 constexpr int SOLVE_ROWS = SOLVE_ROWS_OVERRIDE;  // tools/solve_bench.hip
 #endif
-
-// Sweep step P.  Row P was published (by every wave: its candidate of that
-// local row) into buffer P&1 by the previous step.  All reads are issued
-// first; the row of pivot P+1 is updated before the others and published
-// into the other buffer at once, so the barrier only waits on that.
-template <int RP, int RW, int P>
-__device__ __forceinline__ void sweep_step(double (&a)[RW], double* rowbuf, double* pivs, int c,
-                                           int w) {
-    constexpr int NW = RP / RW, W = P / RW, L = P % RW;
-    const double* row = rowbuf + (P & 1) * NW * 64 + W * 64;  // a_Pc == a_cP
-    const double piv = row[P];
-    const double rc = row[c];
-    double f[RW];  // a_iP for this wave's rows
-#pragma unroll
-    for (int q = 0; q < RW; ++q) f[q] = row[RW * w + q];
-    pivs[P] = piv;  // every thread, same value
-    const double d = 1.0 / piv;
-    const bool pc = (c == P);
-    const double s = rc * d;  // a_Pc / D
-    const double m = pc ? 0.0 : 1.0;
-    const double t = pc ? -d : s;
-    if constexpr (P + 1 < RP) {
-        constexpr int L2 = (P + 1) % RW;
-        a[L2] = m * a[L2] - f[L2] * t;
-        if (L2 == L && w == W) a[L] = t;  // (RW == 1 only)
-        rowbuf[((P + 1) & 1) * NW * 64 + w * 64 + c] = a[L2];
-#pragma unroll
-        for (int q = 0; q < RW; ++q)
-            if (q != L2) a[q] = m * a[q] - f[q] * t;
-    } else {
-#pragma unroll
-        for (int q = 0; q < RW; ++q) a[q] = m * a[q] - f[q] * t;
-    }
-    // row P itself: a_Pc <- a_Pc/D, a_PP <- -1/D
-    if (w == W) a[L] = t;
-    __syncthreads();
-}
-
-template <int RP, int RW, int... Ps>
-__device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, double* pivs, int c,
-                                          int w, std::integer_sequence<int, Ps...>) {
-    (sweep_step<RP, RW, Ps>(a, rowbuf, pivs, c, w), ...);
-}
 
 template <int RP>
 __global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __restrict__ P,

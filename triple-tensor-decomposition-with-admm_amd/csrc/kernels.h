@@ -15,6 +15,18 @@ constexpr int DENSE_SLOTS = 64;
 struct DevState;  // solver.cpp
 
 // ---- K5: fused ADMM update (k_admm.hip) ----------------------------------
+// One R x R solve run by an extra workgroup (blockIdx 0) of K2 or K5
+// (sweep.h: side_solve): Ginv = inv(P o Q + alpha I).  on = 0: none.
+struct SideSolve {
+    const double* P = nullptr;
+    const double* Q = nullptr;
+    double alpha = 0.0;
+    double* Ginv = nullptr;
+    int* flags = nullptr;
+    int R = 0;
+    int on = 0;
+};
+
 struct K5Args {
     const double* D;
     double* O;
@@ -43,6 +55,7 @@ struct K5Args {
     // CP (the executed model): ahj = 0, bhj = RP.  Qi model (opts.model='qi'):
     // Ah = H (k_qi.hip, rows j*n1p+i), ahj = n1p*RP, Bh = ones, bhj = 0.
     int64_t ahj, bhj;
+    SideSolve side;  // RP <= 64, CP model: solve A of the next iteration
 };
 int k5_grid(const Geom& g);
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st);
@@ -72,8 +85,10 @@ void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, c
 int m3_split(const Geom& g);
 int m3_parts(const Geom& g);  // partial slabs of n3p*RP written by K2
 // kr(ij,k) = Ah[j*ahj + i*RP + k] * Bh[j*bhj + k] (K5Args::ahj; bhj < 0 means RP)
+// side: an R x R solve in an extra workgroup of the CP kernel (RP <= 64)
 void launch_m3(const Geom& g, const double* T, const double* Ah, const double* Bh, double* part,
-               double* M3, const int* stop, hipStream_t st, int64_t ahj = 0, int64_t bhj = -1);
+               double* M3, const int* stop, hipStream_t st, int64_t ahj = 0, int64_t bhj = -1,
+               const SideSolve& side = SideSolve{});
 // G = X^T X over `rows` rows of a row-major [rows][RP] factor
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop, hipStream_t st);
 // Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere)

@@ -117,6 +117,13 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     if (!rp_supported32(g_.RP))
         throw Error(TRITD_ERR_UNSUPPORTED, "r must be in 1..16");
     if (qi_ && g_.r > 8) throw Error(TRITD_ERR_UNSUPPORTED, "opts.model='qi': r <= 8");
+    {
+        // one stream, side solves inside K2 / K5 (the cross-stream event of
+        // the side-stream schedules costs ~10 us per sync on the main stream,
+        // tools/sync_bench.hip); TRITD_FUSED=0 keeps the side-stream schedules
+        const char* fe = std::getenv("TRITD_FUSED");
+        fused_ = (overlap_ || shov_) && !qi_ && !f32_ && g_.RP <= 64 && !(fe && std::atoi(fe) == 0);
+    }
 
     // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
     mu_.resize((size_t)o_.maxIter + 2);
@@ -233,7 +240,9 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
 
     // T of iteration 1 (:33) and W = T x3 C0 for update_A/update_B
     if (o_.maxIter > 0) launch_k5_any(1, /*prologue=*/true);
-    if (overlap_ || shov_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
+    if (fused_) {
+        solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, st_);  // solve A of iteration 1
+    } else if (overlap_ || shov_) {  // solve A of iteration 1 (needs the initial B^TB, C^TC)
         TRITD_HIP(hipEventRecord(evCtC_, st_));
         TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
         solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
@@ -443,6 +452,10 @@ void Session::launch_k5_any(int k, bool prologue) {
     a.stop = ctrl_;
     a.dense_tiles = dense_tiles();
     a.rot = rot_;
+    if (!prologue) {
+        a.side = k5side_;
+        k5side_ = SideSolve{};
+    }
     launch_k5(g_, a, prologue, dy_, st_);
 }
 
@@ -631,6 +644,50 @@ void Session::iterate_overlapped(int k) {
     launch_k5_full(k, /*fused_finish=*/true);
 }
 
+// Single-stream iteration (fused_): every kernel on the main stream in
+// dependency order, the two off-critical-path solves inside K2 and K5
+//   M1 -> apply A -> Gram A -> [AR(M2 | A^TA) after M2] -> solve B -> M2 ->
+//   apply B -> Gram B -> K2 (+ solve C) -> [AR(M3)] -> apply C -> Gram C ->
+//   K5 (+ solve A of k+1) -> norms [AR] -> finish
+// (one process per GPU: M2 before solve B, whose A^TA is all-reduced with it)
+void Session::iterate_fused(int k) {
+    const int RP = g_.RP;
+    double* M2 = red1_.p;
+    double* AtA = red1_.p + g_.n2 * RP;
+    do_m1();
+    do_apply_A(GinvA_.p);
+    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    if (comm_ && comm_->comm) {
+        do_m2(M2);
+        allreduce(red1_.p, red1_count());
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+    } else {
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+        do_m2(M2);
+    }
+    do_apply_B(M2, GinvB_.p);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    mark(1);
+    SideSolve sc;  // update_C's solve (:93 ridge) beside K2
+    sc.P = AtA; sc.Q = BtB_.p; sc.alpha = 1e-9; sc.Ginv = GinvC_.p; sc.flags = ctrl_ + 2;
+    sc.R = g_.R; sc.on = 1;
+    launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_, 0, -1, sc);
+    mark(2);
+    allreduce(red2_.p, red2_count());
+    do_apply_C(GinvC_.p);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    // the next update_A's solve (B^TB, C^TC of this iteration) beside K5
+    k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;
+    k5side_.flags = ctrl_ + 2; k5side_.R = g_.R; k5side_.on = 1;
+    if (comm_ && comm_->comm) {
+        launch_k5_full(k, /*fused_finish=*/false);
+        allreduce(red3_.p, 2);
+        phaseD(k);
+    } else {
+        launch_k5_full(k, /*fused_finish=*/true);
+    }
+}
+
 // Sharded iteration (one process per GPU).  The all-reduce
 // of M2 + A^TA gates solve B, which stays on the critical path; the other two
 // solves and the two replicated Grams run on the side stream:
@@ -710,7 +767,9 @@ void Session::run(int iters) {
             ev_iter_.push_back(k);
             mark(0);
         }
-        if (overlap_) {
+        if (fused_) {
+            iterate_fused(k);
+        } else if (overlap_) {
             iterate_overlapped(k);
         } else if (shov_) {
             iterate_sharded(k);

@@ -100,6 +100,13 @@ class Session {
     // one process per GPU with RCCL: the phase order with the Grams of B, C
     // and the solves of C, A(k+1) on the side stream
     void iterate_sharded(int k);
+    // single stream, no events (default for the fp64 CP model at RP <= 64):
+    // the solves of update_C and of the next update_A run in an extra
+    // workgroup of K2 / K5 (sweep.h), solve B on the main stream; with a
+    // communicator the same order with its three all-reduces
+    void iterate_fused(int k);
+    bool fused_ = false;
+    SideSolve k5side_;  // the side solve of the next K5 launch
     bool shov_ = false;
     void create_streams(hipStream_t shared_stream);
     void launch_k5_full(int k, bool fused_finish);

@@ -1,0 +1,95 @@
+// Symmetric Gauss-Jordan sweep of an SPD R x R Gram (k_contract.hip:
+// k_solve, k_solve_ns) and the one-workgroup "side solve" that K2 and K5
+// run in an extra workgroup of their own grid, so the solves
+// of update_C and of the next update_A need no second stream.
+#pragma once
+
+#include <utility>
+
+#include "kernels.h"
+
+namespace tritd {
+
+// Sweep step P.  Row P was published (by every wave: its candidate of that
+// local row) into buffer P&1 by the previous step.  All reads are issued
+// first; the row of pivot P+1 is updated before the others and published
+// into the other buffer at once, so the barrier only waits on that.
+template <int RP, int RW, int P>
+__device__ __forceinline__ void sweep_step(double (&a)[RW], double* rowbuf, double* pivs, int c,
+                                           int w) {
+    constexpr int NW = RP / RW, W = P / RW, L = P % RW;
+    const double* row = rowbuf + (P & 1) * NW * 64 + W * 64;  // a_Pc == a_cP
+    const double piv = row[P];
+    const double rc = row[c];
+    double f[RW];  // a_iP for this wave's rows
+#pragma unroll
+    for (int q = 0; q < RW; ++q) f[q] = row[RW * w + q];
+    pivs[P] = piv;  // every thread, same value
+    const double d = 1.0 / piv;
+    const bool pc = (c == P);
+    const double s = rc * d;  // a_Pc / D
+    const double m = pc ? 0.0 : 1.0;
+    const double t = pc ? -d : s;
+    if constexpr (P + 1 < RP) {
+        constexpr int L2 = (P + 1) % RW;
+        a[L2] = m * a[L2] - f[L2] * t;
+        if (L2 == L && w == W) a[L] = t;  // (RW == 1 only)
+        rowbuf[((P + 1) & 1) * NW * 64 + w * 64 + c] = a[L2];
+#pragma unroll
+        for (int q = 0; q < RW; ++q)
+            if (q != L2) a[q] = m * a[q] - f[q] * t;
+    } else {
+#pragma unroll
+        for (int q = 0; q < RW; ++q) a[q] = m * a[q] - f[q] * t;
+    }
+    // row P itself: a_Pc <- a_Pc/D, a_PP <- -1/D
+    if (w == W) a[L] = t;
+    __syncthreads();
+}
+
+template <int RP, int RW, int... Ps>
+__device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, double* pivs, int c,
+                                          int w, std::integer_sequence<int, Ps...>) {
+    (sweep_step<RP, RW, Ps>(a, rowbuf, pivs, c, w), ...);
+}
+
+// inv(P o Q + alpha I) by the sweep in one 256-thread workgroup: 4 waves of
+// RP/4 rows per lane, lane = column (k_solve's algorithm and rounding with
+// another row split).  rowbuf: 2*4*64 doubles, pivs: RP doubles of LDS.
+// Ginv is written directly (R x R block, zero pad); the pinv-tolerance check
+// of k_solve raises flags[0].
+template <int RP>
+__device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, double* pivs) {
+    constexpr int NW = 4, RW = RP / NW;
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cc = c < RP ? c : 0;  // lanes >= RP read a valid column, never written back
+    double a[RW];
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {
+        const int i = RW * w + q;
+        const bool in = (i < s.R) && (c < s.R);
+        const double pq = s.P[i * RP + cc] * s.Q[i * RP + cc];
+        const double g = (i == c) ? pq + s.alpha : pq;
+        a[q] = in ? g : ((i == c) ? 1.0 : 0.0);
+    }
+    rowbuf[w * 64 + c] = a[0];
+    __syncthreads();
+    sweep_all<RP, RW>(a, rowbuf, pivs, c, w, std::make_integer_sequence<int, RP>{});
+    if (c < RP)
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+            const int i = RW * w + q;
+            s.Ginv[i * RP + c] = (i < s.R && c < s.R) ? -a[q] : 0.0;
+        }
+    if (threadIdx.x == 0) {
+        double minpiv = 1e308, maxpiv = 0.0;
+        for (int p = 0; p < s.R; ++p) {
+            minpiv = fmin(minpiv, pivs[p]);
+            maxpiv = fmax(maxpiv, pivs[p]);
+        }
+        const double tol = (double)s.R * ldexp(1.0, ilogb(maxpiv) - 52);  // pinv: R*eps(max)
+        if (!(minpiv > 1e3 * tol)) atomicOr(s.flags, 1);
+    }
+}
+
+}  // namespace tritd
