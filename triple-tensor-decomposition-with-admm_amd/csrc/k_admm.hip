@@ -53,7 +53,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // faster).
 static constexpr int K5_WAVES = 4;
 #ifndef K5_NT
-#define K5_NT 0  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores
+#define K5_NT 2  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores (round 3: nt stores -1.2 % K5, -1.5 % iteration; nt loads measured slower in round 1)
 #endif
 #ifndef K5_FASTDIV
 #define K5_FASTDIV 1
