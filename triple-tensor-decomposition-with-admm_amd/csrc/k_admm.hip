@@ -53,7 +53,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // faster).
 static constexpr int K5_WAVES = 4;
 #ifndef K5_NT
-#define K5_NT 2  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores (round 3: nt stores -1.2 % K5, -1.5 % iteration; nt loads measured slower in round 1)
+#define K5_NT 3  // nontemporal hints on the streamed tensors: bit 0 loads, bit 1 stores (round 3, interleaved A/B: nt stores -1.5 % iteration, nt loads a further -0.9 %; round 1 had measured nt loads slower)
 #endif
 #ifndef K5_FASTDIV
 #define K5_FASTDIV 1
