@@ -80,8 +80,9 @@ void launch_finish(const double* ss, double normD, int k, double tol, double* er
 // ---- contractions and small linear algebra (k_contract.hip) ---------------
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
                hipStream_t st);
+// side: update_B's R x R solve in an extra workgroup (RP <= 64)
 void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, const int* stop,
-               hipStream_t st);
+               hipStream_t st, const SideSolve& side = SideSolve{});
 int m3_split(const Geom& g);
 int m3_parts(const Geom& g);  // partial slabs of n3p*RP written by K2
 // kr(ij,k) = Ah[j*ahj + i*RP + k] * Bh[j*bhj + k] (K5Args::ahj; bhj < 0 means RP)

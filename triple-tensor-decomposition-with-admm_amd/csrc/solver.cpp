@@ -645,11 +645,11 @@ void Session::iterate_overlapped(int k) {
 }
 
 // Single-stream iteration (fused_): every kernel on the main stream in
-// dependency order, the two off-critical-path solves inside K2 and K5
-//   M1 -> apply A -> Gram A -> [AR(M2 | A^TA) after M2] -> solve B -> M2 ->
-//   apply B -> Gram B -> K2 (+ solve C) -> [AR(M3)] -> apply C -> Gram C ->
-//   K5 (+ solve A of k+1) -> norms [AR] -> finish
-// (one process per GPU: M2 before solve B, whose A^TA is all-reduced with it)
+// dependency order, the R x R solves inside the launches they run beside
+//   M1 -> apply A -> Gram A -> M2 (+ solve B) -> apply B -> Gram B ->
+//   K2 (+ solve C) -> apply C -> Gram C -> K5 (+ solve A of k+1) -> norms
+// One process per GPU: M2 -> AR(M2 | A^TA) -> solve B (k_solve_ns, main),
+// AR(M3) after K2, AR(norms) after K5.
 void Session::iterate_fused(int k) {
     const int RP = g_.RP;
     double* M2 = red1_.p;
@@ -662,8 +662,11 @@ void Session::iterate_fused(int k) {
         allreduce(red1_.p, red1_count());
         solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
     } else {
-        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
-        do_m2(M2);
+        // update_B's solve (A^TA of this iteration, C^TC) beside M2
+        SideSolve sb;
+        sb.P = AtA; sb.Q = CtC_.p; sb.alpha = o_.lambda2; sb.Ginv = GinvB_.p; sb.flags = ctrl_ + 2;
+        sb.R = g_.R; sb.on = 1;
+        launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_, sb);
     }
     do_apply_B(M2, GinvB_.p);
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);

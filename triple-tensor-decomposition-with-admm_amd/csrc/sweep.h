@@ -60,6 +60,8 @@ __device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, doubl
 // of k_solve raises flags[0].
 template <int RP>
 __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, double* pivs) {
+    // the host kernel's other workgroups share this CU's SIMDs: win issue
+    __builtin_amdgcn_s_setprio(3);
     constexpr int NW = 4, RW = RP / NW;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int cc = c < RP ? c : 0;  // lanes >= RP read a valid column, never written back
