@@ -55,6 +55,39 @@ def test_rccl_single_rank_session(tritd):
                orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
 
 
+def test_rccl_session_batches_and_disp(tritd):
+    """With a communicator each iteration's stop test rides on the next
+    iteration's first all-reduce (Session::iterate_fused) and run() ends with
+    a standalone one: stepping in uneven batches, and printing every 10
+    iterations, give the one-batch results bitwise and the reference's lines."""
+    import tritd_oracle as orc
+    g = load_golden("g30_r3")
+    n1, n2, n3 = g["D"].shape
+    opts = dict(g["opts"], disp=1, maxIter=23)
+    outs, printed = [], []
+    for batches in ((23,), (7, 1, 10, 5)):
+        lines = []
+        tritd.set_printer(lines.append)
+        try:
+            comm = tritd.Comm(tritd.Comm.unique_id(), 1, 0, 0)
+            s = tritd.Session(g["r"], opts, g["A0"], g["B0"], g["C0"], n1=n1, n2=n2, n3=n3,
+                              D=g["D"], device=0, comm=comm)
+            for b in batches:
+                s.run(b)
+            outs.append(s.get())
+            s.close()
+            comm.close()
+        finally:
+            tritd.set_printer(None)
+        printed.append(lines)
+    ref_lines = []
+    orc.triple_decomp_ADMM(g["D"], g["r"], opts, g["A0"], g["B0"], g["C0"], printer=ref_lines.append)
+    assert printed[0] == printed[1] == ref_lines
+    assert outs[0]["k"] == outs[1]["k"] == 23
+    for key in ("A", "B", "C", "O", "E", "errHist"):
+        np.testing.assert_array_equal(outs[0][key], outs[1][key])
+
+
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_single_gpu_schedules_match_golden(tritd, fused, monkeypatch):
     """TRITD_FUSED=1 (default): one stream, solves of C and A(k+1) inside

@@ -164,8 +164,14 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     Wk_.alloc_bytes((size_t)g_.RP * g_.plane * es_);
     TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.bytes(), st_));
     if (f32_) ChF_.alloc_bytes((size_t)g_.n3p * g_.RP * sizeof(float));
-    Ah_.alloc(g_.n1p * g_.RP);
-    AhT_.alloc((size_t)g_.RP * g_.n1p);
+    for (int q = 0; q < 2; ++q) {
+        AhB_[q].alloc(g_.n1p * g_.RP);
+        AhTB_[q].alloc((size_t)g_.RP * g_.n1p);
+        TRITD_HIP(hipMemsetAsync(AhB_[q].p, 0, AhB_[q].bytes(), st_));
+        TRITD_HIP(hipMemsetAsync(AhTB_[q].p, 0, AhTB_[q].bytes(), st_));
+    }
+    Ah_.owned = AhT_.owned = false;
+    set_ah(0);  // the initial factors go to parity 0 (k done = 0)
     Bh_.alloc(g_.n2 * g_.RP);
     Ch_.alloc(g_.n3p * g_.RP);
     ChT_.alloc((size_t)g_.RP * g_.n3p);
@@ -185,7 +191,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         launch_fill(ones_.p, (int64_t)ones_.n, 1.0, st_);
         for (DBuf* b : {&GqA_, &GqB_, &GqC_}) b->alloc((size_t)g_.RP * g_.RP);
     }
-    red1_.alloc(red1_count());
+    red1_.alloc(red1_count() + 2 * (size_t)k5_grid(g_));  // + the tail for K5's norm partials
     red2_.alloc(red2_count());
     red3_.alloc(2);
     k5part_.alloc(2 * (size_t)k5_grid(g_));
@@ -440,7 +446,8 @@ void Session::launch_k5_any(int k, bool prologue) {
     // E^(k-1) is read, E^(k) written (dy: over E^(k-2); otherwise in place)
     a.E = e_buf(k - 1); a.CE = ce_buf(k - 1);
     a.Ep = e_buf(k); a.CEp = ce_buf(k);
-    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p; a.partial = k5part_.p;
+    a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p;
+    a.partial = (k5part_to_ && !prologue) ? k5part_to_ : k5part_.p;
     a.ahj = 0; a.bhj = g_.RP;
     if (qi_) {  // L = H Ch^T (H built before K2 of this iteration)
         a.Ah = H_.p; a.Bh = ones_.p;
@@ -468,7 +475,25 @@ void Session::allreduce(double* buf, int64_t count) {
 
 int Session::next_iter() {
     if (k_enq_ >= o_.maxIter) return 0;
-    return ++k_enq_;
+    ++k_enq_;
+    set_ah(k_enq_);
+    return k_enq_;
+}
+
+void Session::set_ah(int k) {
+    Ah_.p = AhB_[k & 1].p;
+    Ah_.n = AhB_[k & 1].n;
+    AhT_.p = AhTB_[k & 1].p;
+    AhT_.n = AhTB_[k & 1].n;
+}
+
+void Session::flush_norms() {
+    if (!norms_pending_) return;
+    double* parts = red1_.p + red1_count();
+    allreduce(parts, 2 * (int64_t)k5_grid(g_));
+    launch_reduce_finish(parts, k5_grid(g_), normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
+                         ctrl_, f32_, st_);
+    norms_pending_ = false;
 }
 
 void Session::phaseA(int k) {
@@ -659,7 +684,17 @@ void Session::iterate_fused(int k) {
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
     if (comm_ && comm_->comm) {
         do_m2(M2);
-        allreduce(red1_.p, red1_count());
+        // M1 .. M2 above ran before the stop test of iteration k-1: they
+        // write only scratch and this iteration's A^ parity buffer.  The
+        // all-reduce carries K5(k-1)'s norm partials; the finish of k-1
+        // follows it, and every kernel after that checks its stop flag.
+        const bool pend = norms_pending_;
+        allreduce(red1_.p, red1_count() + (pend ? 2 * (int64_t)k5_grid(g_) : 0));
+        if (pend) {
+            launch_reduce_finish(red1_.p + red1_count(), k5_grid(g_), normD_, pend_k_, o_.tol,
+                                 errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_);
+            norms_pending_ = false;
+        }
         solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
     } else {
         // update_B's solve (A^TA of this iteration, C^TC) beside M2
@@ -683,9 +718,15 @@ void Session::iterate_fused(int k) {
     k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;
     k5side_.flags = ctrl_ + 2; k5side_.R = g_.R; k5side_.on = 1;
     if (comm_ && comm_->comm) {
-        launch_k5_full(k, /*fused_finish=*/false);
-        allreduce(red3_.p, 2);
-        phaseD(k);
+        // the norm partials stay per workgroup in red1_'s tail: all-reduced
+        // with the next iteration's M2 | A^TA (or by flush_norms)
+        k5part_to_ = red1_.p + red1_count();
+        mark(3);
+        launch_k5_any(k, /*prologue=*/false);
+        mark(4);
+        k5part_to_ = nullptr;
+        norms_pending_ = true;
+        pend_k_ = k;
     } else {
         launch_k5_full(k, /*fused_finish=*/true);
     }
@@ -740,6 +781,7 @@ void Session::phaseD(int k) {
 
 void Session::maybe_print(int k) {
     if (!o_.disp || k % 10 != 0) return;
+    flush_norms();
     if (comm_ && comm_->rank != 0) return;
     int ctrl[2];
     double eL, eO;
@@ -788,6 +830,7 @@ void Session::run(int iters) {
         mark(5);
         maybe_print(k);
     }
+    flush_norms();  // the last iteration's stop test (errHist complete after every run)
 }
 
 void Session::harvest_timing() {
@@ -843,9 +886,10 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
                   double* errHist, int* iters) {
     int done = 0, stopped = 0;
     sync(&done, &stopped);
-    if (A) {
-        std::vector<double> h(Ah_.n);
-        TRITD_HIP(hipMemcpy(h.data(), Ah_.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (A) {  // the A of the last finished iteration (its parity buffer)
+        const DBuf& a = AhB_[done & 1];
+        std::vector<double> h(a.n);
+        TRITD_HIP(hipMemcpy(h.data(), a.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
         unpack_A(g_, h, A);
     }
     if (B) {
@@ -914,13 +958,16 @@ void Session::rre_parts(const void* dX, int64_t ldX, double* num, double* den) {
     const int grid = tp_grid(g_);
     part.alloc(2 * (size_t)grid);
     out.alloc(2);
+    int done = 0;
+    sync(&done, nullptr);
+    const double* ah = AhB_[done & 1].p;  // the A of the last finished iteration
     // X(i,j,t) of the shard at src[i + ldX*(j + n2*t)]
     if (qi_) {
-        launch_qi_h(g_, g_.r, Ah_.p, Bh_.p, H_.p, nullptr, st_);
+        launch_qi_h(g_, g_.r, ah, Bh_.p, H_.p, nullptr, st_);
         launch_tp(g_, H_.p, ones_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_,
                   g_.n1p * g_.RP, 0);
     } else {
-        launch_tp(g_, Ah_.p, Bh_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_);
+        launch_tp(g_, ah, Bh_.p, ChT_.p, nullptr, src, part.p, 1, ldX, ldX * g_.n2, st_);
     }
     launch_reduce_pairs(part.p, grid, out.p, nullptr, st_);
     double h[2];

@@ -107,6 +107,13 @@ class Session {
     void iterate_fused(int k);
     bool fused_ = false;
     SideSolve k5side_;  // the side solve of the next K5 launch
+    // communicator: K5's norm partials of iteration pend_k_ wait in red1_'s
+    // tail for the next iteration's first all-reduce (one all-reduce fewer
+    // per iteration); flush_norms() all-reduces and finishes them alone
+    bool norms_pending_ = false;
+    int pend_k_ = 0;
+    double* k5part_to_ = nullptr;  // where the next K5 writes its partials (null: k5part_)
+    void flush_norms();
     bool shov_ = false;
     void create_streams(hipStream_t shared_stream);
     void launch_k5_full(int k, bool fused_finish);
@@ -158,7 +165,13 @@ class Session {
     DBuf CE2_;
     double* ce_buf(int k) const { return (dy_ && (k & 1)) ? CE2_.p : CE_.p; }
     double* e_buf(int k) const { return (dy_ && (k & 1)) ? YO_.p : E_.p; }
+    // A^ (and its transpose) by iteration parity: iteration k writes
+    // AhB_[k&1], so the A of the last finished iteration survives a next
+    // iteration that has already started (the speculative start of
+    // iterate_fused with a communicator); Ah_/AhT_ are views of the current one
+    DBuf AhB_[2], AhTB_[2];
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, BtB_, CtC_;
+    void set_ah(int k);
     // Qi model (opts.model = TRITD_MODEL_QI, k_qi.hip): H = the Qi mode-3 design
     // matrix by rows ij (K2/K5 Khatri-Rao operand), an all-ones RP x RP block
     // (the Hadamard factor of the solve and the B operand of the KR product),
