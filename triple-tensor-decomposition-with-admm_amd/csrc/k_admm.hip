@@ -42,6 +42,7 @@
 // is compiled with -ffp-contract=off so no statement is fused into an FMA.
 #include "kernels.h"
 #include "sweep.h"
+#include "wtrace.h"
 
 namespace tritd {
 
@@ -95,6 +96,9 @@ static constexpr int K5_WAVES = 4;
 #define K5_WPE 2  // waves per SIMD at RP <= 64 (one wave: 1.243 vs 0.998 ms, round 3)
 #endif
 
+#if TRITD_WTRACE
+WT_DECL(g_wt_k5)
+#endif
 #if K5_PROF
 // phase clocks of the t-walk summed over waves: [0..7] phases, [8] steps
 __device__ unsigned long long g_k5prof[16];
@@ -282,6 +286,7 @@ void k5_fused(K5Args a) {
         }
     }
     const int64_t bid = (int64_t)blockIdx.x - side;  // this workgroup's group of ij-tiles
+    WT_BEGIN();
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
     constexpr int LDC = RP + 16; // row stride of the [t][k] C^ slice (2*LDC = 32 mod 64: no bank conflicts)
@@ -816,6 +821,7 @@ void k5_fused(K5Args a) {
             a.partial[2 * bid + 1] = y;
         }
     }
+    WT_END(g_wt_k5, PRO ? -1 : bid * K5_WAVES + (threadIdx.x >> 6));
 }
 
 int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }

@@ -16,6 +16,7 @@
 
 #include "kernels.h"
 #include "sweep.h"
+#include "wtrace.h"
 
 namespace tritd {
 
@@ -334,6 +335,9 @@ __global__ __launch_bounds__(256, 2) void k_m3(const double* __restrict__ T,
 // exposed the HBM latency every ij-tile.)
 // Wave = (t-block of 64 t, i-tile, part jp of the fibres); S waves per
 // t-block (padded to a multiple of 4, surplus waves contribute zeros).
+#if TRITD_WTRACE
+WT_DECL(g_wt_k2)
+#endif
 template <int RP, int LDA>
 __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
                                                   const double* __restrict__ Ah,
@@ -349,6 +353,7 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
         return;
     }
     const int64_t bid = (int64_t)blockIdx.x - side.on;
+    WT_BEGIN();
     // the second workgroup a CU receives starts later, so that the two waves
     // sharing each SIMD are out of phase (their copy/wait boundaries would
     // otherwise leave the matrix pipe idle together)
@@ -480,6 +485,7 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
                     if (t < n3p) out[t * LDA + k] = v;
                 }
     }
+    WT_END(g_wt_k2, bid * 4 + wid);
 }
 
 // M3[t][k] = sum_y part[y][t][k]  (fixed order); 4 slices per output summed in LDS

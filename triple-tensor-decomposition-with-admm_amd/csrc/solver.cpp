@@ -123,6 +123,8 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         // tools/sync_bench.hip); TRITD_FUSED=0 keeps the side-stream schedules
         const char* fe = std::getenv("TRITD_FUSED");
         fused_ = (overlap_ || shov_) && !qi_ && !f32_ && g_.RP <= 64 && !(fe && std::atoi(fe) == 0);
+        const char* ks = std::getenv("TRITD_K2SIDE");
+        k2side_ = ks ? std::atoi(ks) : 1;
     }
 
     // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
@@ -708,9 +710,10 @@ void Session::iterate_fused(int k) {
     mark(1);
     SideSolve sc;  // update_C's solve (:93 ridge) beside K2
     sc.P = AtA; sc.Q = BtB_.p; sc.alpha = 1e-9; sc.Ginv = GinvC_.p; sc.flags = ctrl_ + 2;
-    sc.R = g_.R; sc.on = 1;
+    sc.R = g_.R; sc.on = k2side_ != 0;
     launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_, 0, -1, sc);
     mark(2);
+    if (!sc.on) solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, st_);
     allreduce(red2_.p, red2_count());
     do_apply_C(GinvC_.p);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);

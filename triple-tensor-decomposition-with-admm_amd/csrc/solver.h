@@ -106,6 +106,7 @@ class Session {
     // communicator the same order with its three all-reduces
     void iterate_fused(int k);
     bool fused_ = false;
+    int k2side_ = 1;  // update_C's solve beside K2 (0: after it, experiments)
     SideSolve k5side_;  // the side solve of the next K5 launch
     // communicator: K5's norm partials of iteration pend_k_ wait in red1_'s
     // tail for the next iteration's first all-reduce (one all-reduce fewer
