@@ -2,9 +2,9 @@
 (SURVEY.md §8e).
 
 Each rank owns rows i in [i0, i1) of D (and of O, E, Y_L, Y_O, T, A^).
-B^ and C^ are replicated.  Per iteration libtritd issues three RCCL
-all-reduces on its own stream (M2 | A^TA, M3, the two residual norms); the
-only host-side collective is the broadcast of the 128-byte RCCL unique id
+B^ and C^ are replicated.  Per iteration libtritd issues two RCCL
+all-reduces on its own stream (M2 | A^TA with the previous iteration's
+residual-norm partials in its tail, then M3); the only host-side collective is the broadcast of the 128-byte RCCL unique id
 at start-up, done here over torch.distributed.
 """
 from __future__ import annotations
