@@ -1,0 +1,7 @@
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/c5probe; mkdir -p $O
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
+    python3 bench.py --config 5 --no-cpu --steps 10 --warmup 3 > $O/stats.log 2>&1
+timeout -s KILL 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d $O/p1 -o run -- \
+    python3 bench.py --config 5 --no-cpu --steps 3 --warmup 1 > $O/p1.log 2>&1
