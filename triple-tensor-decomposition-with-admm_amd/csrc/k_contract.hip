@@ -504,10 +504,10 @@ __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ pa
 }
 
 // total waves of one K2 launch (TRITD_M3_WAVES: experiments): about two per SIMD
-static int64_t m3_waves() {
+static int64_t m3_waves() {  // TRITD_M3_WAVES (experiments); 0: the CP kernel's own choice
     static const int64_t waves = [] {
         const char* e = std::getenv("TRITD_M3_WAVES");
-        return e ? (int64_t)std::atoll(e) : (int64_t)2048;
+        return e ? (int64_t)std::atoll(e) : (int64_t)0;
     }();
     return waves;
 }
@@ -515,7 +515,7 @@ static int64_t m3_waves() {
 // generic kernel: waves per t-block (multiple of 4)
 int m3_split(const Geom& g) {
     const int64_t ntb = cdiv(g.ntt, 4);
-    int64_t S = m3_waves() / ntb;
+    int64_t S = (m3_waves() > 0 ? m3_waves() : 2048) / ntb;
     if (S > g.tiles) S = g.tiles;
     S = (S + 3) / 4 * 4;
     if (S < 4) S = 4;
@@ -531,7 +531,19 @@ static M3Cp m3_cp_split(const Geom& g) {
     M3Cp c;
     c.qper = g.n1p >> 4;
     const int64_t ntb = cdiv(g.ntt, 4);
-    int64_t J = m3_waves() / (ntb * c.qper);
+    // about two waves per SIMD while that leaves every wave >= 64 fibre steps
+    // (the whole 512^3 problem); shorter walks (mode-1 shards of 256 rows
+    // and less) run one wave per SIMD: the prologue, the reduction epilogue
+    // and the partial slabs are per wave, and the grid then leaves room for
+    // the side solve's workgroup instead of displacing a compute one
+    // (shard timings, 64-row shard: K2 + reduce 63.9 -> 55.8 us; 128 rows
+    // 97.3 -> 88.0; 256 rows 161 -> 157; 512 rows 2048 waves stay ~1 % ahead)
+    int64_t waves = m3_waves();
+    if (waves <= 0) {
+        const int64_t J2 = 2048 / (ntb * c.qper);
+        waves = (J2 >= 1 && g.n2 / J2 >= 64) ? 2048 : 1024;
+    }
+    int64_t J = waves / (ntb * c.qper);
     if (J < 1) J = 1;
     if (J > g.n2) J = g.n2;
     c.J = J;
