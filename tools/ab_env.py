@@ -9,7 +9,13 @@ from tritd import synth
 var, vals, reps = sys.argv[1], sys.argv[2].split(","), int(sys.argv[3])
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 n, r = 512, 8
-if os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere
+n1 = n2 = n3 = n
+if os.environ.get("AB_CFG", "4") == "5":  # 2048x2048x256 r=16 fp32 (bench.py --config 5)
+    n1, n2, n3, r = 2048, 2048, 256, 16
+    dd = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    D, A0, B0, C0 = dd["D"].astype(np.float32, order="F"), dd["A0"], dd["B0"], dd["C0"]
+    del dd
+elif os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere
     rng = np.random.default_rng(0)
     D = np.asfortranarray(rng.standard_normal((n, n, n)))
     A0, B0, C0 = synth.random_factors(n, n, n, r, 123)
@@ -21,8 +27,8 @@ res = {v: [] for v in vals}
 for rep in range(reps):
     for v in vals:
         os.environ[var] = v
-        s = tritd.Session(r, opts, A0, B0, C0, n1=n, n2=n, n3=n, D=D, device=0)
-        s.run(15); s.sync(); s.set_timing(True); s.run(iters); s.sync()
+        s = tritd.Session(r, opts, A0, B0, C0, n1=n1, n2=n2, n3=n3, D=D, device=0, dtype=D.dtype)
+        s.run(int(os.environ.get('AB_WARM', '15'))); s.sync(); s.set_timing(True); s.run(iters); s.sync()
         km = s.kernel_ms()
         res[v].append((km["iteration"], km["fused_update"], km["mode3"]))
         print("%s=%s rep %d: it %.3f k5 %.3f m3 %.3f" % (var, v, rep, km["iteration"], km["fused_update"], km["mode3"]), flush=True)

@@ -14,7 +14,7 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch
     $B > $O/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- \
     $B > $O/pmc_write.log 2>&1
-python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/${TAG}_c5_k5_traffic.json $ALG "k5_f32<256, false>" 1:4  # timed window (warmup 1, steps 3): E densifies later
+python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/${TAG}_c5_k5_traffic.json $ALG "k5_f32s<256>" 1:4  # timed window (warmup 1, steps 3): E densifies later
 cp $O/${TAG}_c5_k5_traffic.json profiles/${TAG}_c5_k5_traffic.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
     python3 bench.py --config 5 --no-cpu --steps 10 --warmup 3 > $O/stats.log 2>&1

@@ -17,6 +17,9 @@
 // l: words 0..7 are the four 64-bit ballot masks (mask w <=> register element
 // w of every lane), words 8..63 the nonzeros in (w, lane) order; more than 56
 // nonzeros -> the tile is stored densely in E and its masks are all ones.
+#include <cstdlib>
+#include <type_traits>
+
 #include "kernels.h"
 
 // K5F_EXP (timing experiments only, results invalid): 1 no W MFMAs, 2 no L
@@ -429,7 +432,269 @@ void k5_f32(K5Args32 a) {
     }
 }
 
+// RP = 256 with the rank split over a wave pair (K5F_SPLIT, default): two
+// waves share each ij-tile, wave h of the pair holding the K-steps
+// s in [h*KS/2, (h+1)*KS/2) of the L operand (k = (l>>4) * KS + s) and the
+// W M-tiles m = 4q + u of granules q in [h*G/2, (h+1)*G/2).  Per t-tile each
+// forms its half of L, the pair adds the halves through LDS (both in the same
+// order: both waves then hold bitwise the same L), both run the elementwise
+// chain (wave 0 stores Y_L, Y_O, T, E and sums the norms), and each
+// accumulates its half of W.  Half the L operands and W accumulators per
+// wave fit two waves per SIMD, which the one-wave kernel (352 VGPRs) could
+// not: at one wave per SIMD a t-tile step took ~8 800 cycles against ~5 200
+// of issue.
+template <int RP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k5_f32s(K5Args32 a) {
+    static_assert(RP % 128 == 0, "k5_f32s: RP = 128 or 256");
+    if (*a.stop) return;
+    constexpr int KS = RP / 4, MT = RP / 16, LDC = RP + 4;
+    constexpr int G = MT / 4, GH = G / 2, KSH = KS / 2, MTH = MT / 2;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int slot = wid >> 1;  // ij-tile of the pair within the workgroup
+    const int il = lane & 15, tg = lane >> 4;
+    const int64_t tile = (int64_t)blockIdx.x * 2 + slot;
+    const bool active = tile < a.tiles;
+    const int64_t qper = a.n1p >> 4;
+    const int64_t j = active ? tile / qper : 0;
+    const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
+    const int64_t ntt = a.ntt;
+    auto gran = [](int c, int q) { return c * G + ((q + ((c * G) >> 4)) & (G - 1)); };
+    __shared__ __attribute__((aligned(16))) float sC[2][16 * LDC];
+    __shared__ float tsm[2][16 * 17];
+    __shared__ float csm[2][128];
+    __shared__ __attribute__((aligned(16))) f4 lx[2][2][64];  // [slot][half] partial L
+    float* ts = tsm[slot];
+    float* cs = csm[slot];
+    constexpr int WS = RP * 16 + 16;
+    static_assert(2 * WS <= 2 * 16 * LDC, "k5_f32s: the W exchange reuses the C^ slices");
+
+    constexpr int SQ = 16 * RP / 4;
+    constexpr int NS = SQ / 256;
+    static_assert(SQ % 256 == 0, "k5_f32s: staging");
+    f4 sv[NS];
+    auto stage_load = [&](int64_t tt) {
+        const f4* src = reinterpret_cast<const f4*>(a.ChF + (tt << 4) * RP);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) sv[q] = src[threadIdx.x + q * 256];
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * 256;
+            const int row = (4 * e) / RP, k = (4 * e) % RP;
+            *reinterpret_cast<f4*>(&sC[buf][row * LDC + 4 * gran((k >> 2) / G, (k >> 2) % G)]) = sv[q];
+        }
+    };
+    const IterScalars32 sc = a.s;
+    const f4* D4 = reinterpret_cast<const f4*>(a.D);
+    f4* E4 = reinterpret_cast<f4*>(a.E);
+    f4* YL4 = reinterpret_cast<f4*>(a.YL);
+    f4* YO4 = reinterpret_cast<f4*>(a.YO);
+    f4* T4 = reinterpret_cast<f4*>(a.T);
+    struct Regs {
+        f4 x[3];
+        f4 ed;
+        float ce;
+    };
+    auto tbase = [&](int64_t tt) { return tm_tile_base(tile, tt, ntt); };
+    auto load = [&](int64_t tt, Regs& nx) {
+        const int64_t o = (tbase(tt) >> 2) + lane;
+        nx.x[0] = D4[o];
+        nx.x[1] = YL4[o];
+        nx.x[2] = YO4[o];
+    };
+    auto load_dense = [&](int64_t tt, Regs& nx) { nx.ed = E4[(tbase(tt) >> 2) + lane]; };
+    auto load_slot = [&](int64_t tt, float& ce) {
+        const int64_t t2 = tt < ntt ? tt : ntt - 1;
+        ce = a.CE[(tbase(t2) >> 8) * CE32_SLOT + lane];
+    };
+    double ssL = 0.0, ssO = 0.0;
+    unsigned ndense = 0;
+    f4 wacc[MTH];
+
+    // the walk, specialised per half (straight-line code in each)
+    auto walk = [&](auto HC) {
+        constexpr int h = decltype(HC)::value;
+        float kr[KSH];  // KR(ij = l & 15, k = (l>>4) * KS + h*KSH + s), single-rounded
+#pragma unroll
+        for (int s = 0; s < KSH; ++s) {
+            const int k = tg * KS + h * KSH + s;
+            kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
+        }
+#pragma unroll
+        for (int m = 0; m < MTH; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+            const int64_t tb = tbase(tt);
+            const int64_t o = (tb >> 2) + lane;
+            if (pf) {
+                const bool dn1 = ce32_is_dense(nx.ce);
+                stage_load(tt + 1);
+                load(tt + 1, nx);
+                __builtin_amdgcn_sched_barrier(0);
+                if (dn1) load_dense(tt + 1, nx);
+            }
+            float ev[4];
+            const bool dn = ce32_decode(cx.ce, lane, ev);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
+            if (pf) load_slot(tt + 2, cx.ce);
+            const float* cR = sC[buf];
+            f4 lacc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+            const f4* cL = reinterpret_cast<const f4*>(cR + il * LDC);
+#pragma unroll
+            for (int s4 = 0; s4 < KSH / 4; ++s4) {
+                const int gl = tg * (KS / 4) + h * (KSH / 4) + s4;
+                const f4 c = cL[gran(gl / G, gl % G)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+            }
+            lx[slot][h][lane] = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
+            __syncthreads();
+            const f4 Lv = lx[slot][0][lane] + lx[slot][1][lane];  // same order in both waves
+            float En[4], tr[4];
+            f4 YLn, YOn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = cx.x[0][r], yl = cx.x[1][r], yo = cx.x[2][r], e = ev[r];
+                const float L = Lv[r];
+                const float R1 = (d - L) + sc.invL * yl;               // :41
+                const float R2 = e - sc.invO * yo;                     // :42
+                const float Onum = sc.muL * R1 + sc.muO * R2;
+                const float q0 = Onum * sc.rden;
+                const float On = fmaf(fmaf(-q0, sc.den, Onum), sc.rden, q0);  // :43
+                const float R3 = On + sc.invO * yo;                    // :46
+                const float Ev = R3 - fminf(fmaxf(R3, -sc.thr), sc.thr);  // :47
+                const float rL = (d - L) - On;                         // :50
+                const float rO = On - Ev;                              // :51
+                const float yln = yl + sc.muL * rL;                    // :52
+                const float yon = yo + sc.muO * rO;                    // :53
+                tr[r] = (d - On) + sc.invL_next * yln;                 // :33 (k+1)
+                if (h == 0) {
+                    ssL = fma((double)rL, (double)rL, ssL);
+                    ssO = fma((double)rO, (double)rO, ssO);
+                }
+                En[r] = Ev;
+                YLn[r] = yln;
+                YOn[r] = yon;
+            }
+            if (h == 0) {
+                YL4[o] = YLn;
+                YO4[o] = YOn;
+                ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), ndense);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ts[(4 * tg + r) * 17 + il] = tr[r];
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                f4 tv;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) tv[s] = ts[il * 17 + 4 * s + tg];
+                T4[o] = tv;
+            }
+            // this half's W M-tiles: granules q in [h*GH, (h+1)*GH)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
+#pragma unroll
+                for (int q = 0; q < GH; ++q) {
+                    const f4 c = cW[gran(il, h * GH + q)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
+                }
+            }
+            if (pf) stage_store(buf ^ 1);
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        Regs xa, xb;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xa.x[q] = xb.x[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        xa.ed = xb.ed = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        load_slot(0, xa.ce);
+        load_slot(1, xb.ce);
+        load(0, xa);
+        if (ce32_is_dense(xa.ce)) load_dense(0, xa);
+        stage_load(0);
+        stage_store(0);
+        __syncthreads();
+        int64_t tt = 0;
+        for (; tt + 2 < ntt; tt += 2) {
+            body(tt, 0, xa, xb, true);
+            body(tt + 1, 1, xb, xa, true);
+        }
+        if (tt + 1 < ntt) {
+            body(tt, 0, xa, xb, true);
+            body(tt + 1, 1, xb, xa, false);
+        } else {
+            body(tt, 0, xa, xb, false);
+        }
+        // W^T C/D layout: M-tile m row rho = 4(l>>4) + rr, col ij = l & 15,
+        // k = rho * MT + m; this half's m = 4(h*GH + q) + u
+        float* wl = &sC[0][0];  // the C^ slices are dead after the walk
+        __syncthreads();
+#pragma unroll
+        for (int mq = 0; mq < MTH; ++mq)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int m = 4 * h * GH + mq;
+                const int k = (4 * tg + rr) * MT + m;
+                wl[slot * WS + k * 16 + il] = wacc[mq][rr];
+            }
+    };
+    if (wid & 1)
+        walk(std::integral_constant<int, 1>{});
+    else
+        walk(std::integral_constant<int, 0>{});
+    __syncthreads();
+    {
+        // two adjacent ij-tiles = 32 consecutive ij: each lane half of a wave
+        // stores one 128 B row piece of a k-plane
+        const int64_t t0 = (int64_t)blockIdx.x * 2;
+        const int sl = (lane >> 4) & 1;
+        const bool ok = t0 + sl < a.tiles;
+        float* wl = &sC[0][0];
+        float* dst = a.Wk + (t0 << 4) + 16 * sl + il;
+#pragma unroll 4
+        for (int k0 = 2 * wid; k0 < RP; k0 += 8) {
+            const int k = k0 + (lane >> 5);
+            if (ok) dst[(int64_t)k * a.plane] = wl[sl * WS + k * 16 + il];
+        }
+    }
+    if ((wid & 1) == 0 && ndense && lane == 0)
+        atomicAdd(a.dense_tiles + ((blockIdx.x * 2 + slot) & (DENSE_SLOTS - 1)), (unsigned long long)ndense);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        ssL += __shfl_xor(ssL, off);
+        ssO += __shfl_xor(ssO, off);
+    }
+    __shared__ double red[2][4];
+    if (lane == 0) {
+        red[0][wid] = ssL;  // 0 for the odd waves
+        red[1][wid] = ssO;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.partial[2 * blockIdx.x] = red[0][0] + red[0][2];
+        a.partial[2 * blockIdx.x + 1] = red[1][0] + red[1][2];
+    }
+}
+
+bool k5_split32(const Geom& g) {
+    if (g.RP != 256) return false;
+    const char* e = std::getenv("TRITD_K5F_SPLIT");
+    return !(e && std::atoi(e) == 0);
+}
+int k5_parts32(const Geom& g) { return k5_split32(g) ? (int)cdiv(g.tiles, 2) : k5_grid(g); }
+
 void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st) {
+    if (!prologue && k5_split32(g)) {
+        hipLaunchKernelGGL(k5_f32s<256>, dim3((unsigned)k5_parts32(g)), dim3(256), 0, st, a);
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     const dim3 grid(k5_grid(g)), block(64 * K5W);
 #define K5F_CASE(RPV)                                                        \
     case RPV:                                                                \

@@ -58,6 +58,7 @@ struct K5Args {
     SideSolve side;  // RP <= 64, CP model: solve A of the next iteration
 };
 int k5_grid(const Geom& g);
+int k5_parts32(const Geom& g);  // fp32 K5's norm-partial count (its workgroups)
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st);
 // O_k = (D + invL_next*Y_L) - T_{k+1} (O is not stored by K5)
 void launch_pool_probe(const Geom& g, double* D, double* YL, double* YO, double* T, double* CE,

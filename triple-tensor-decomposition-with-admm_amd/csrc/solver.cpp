@@ -193,10 +193,10 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         launch_fill(ones_.p, (int64_t)ones_.n, 1.0, st_);
         for (DBuf* b : {&GqA_, &GqB_, &GqC_}) b->alloc((size_t)g_.RP * g_.RP);
     }
-    red1_.alloc(red1_count() + 2 * (size_t)k5_grid(g_));  // + the tail for K5's norm partials
+    red1_.alloc(red1_count() + 2 * (size_t)k5n());  // + the tail for K5's norm partials
     red2_.alloc(red2_count());
     red3_.alloc(2);
-    k5part_.alloc(2 * (size_t)k5_grid(g_));
+    k5part_.alloc(2 * (size_t)k5n());
     m3part_.alloc((size_t)(f32_ ? m3_parts32(g_) : m3_parts(g_)) * g_.n3p * g_.RP);
     sqpart_.alloc(2 * (size_t)sumsq_blocks(g_));
     const size_t mi = o_.maxIter > 0 ? (size_t)o_.maxIter : 1;
@@ -492,8 +492,8 @@ void Session::set_ah(int k) {
 void Session::flush_norms() {
     if (!norms_pending_) return;
     double* parts = red1_.p + red1_count();
-    allreduce(parts, 2 * (int64_t)k5_grid(g_));
-    launch_reduce_finish(parts, k5_grid(g_), normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
+    allreduce(parts, 2 * (int64_t)k5n());
+    launch_reduce_finish(parts, k5n(), normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
                          ctrl_, f32_, st_);
     norms_pending_ = false;
 }
@@ -606,10 +606,10 @@ void Session::launch_k5_full(int k, bool fused_finish) {
     launch_k5_any(k, /*prologue=*/false);
     mark(4);
     if (fused_finish)  // single GPU: no all-reduce between the norm sums and the stop test
-        launch_reduce_finish(k5part_.p, k5_grid(g_), normD_, k, o_.tol, errHist_.p, errL_.p,
+        launch_reduce_finish(k5part_.p, k5n(), normD_, k, o_.tol, errHist_.p, errL_.p,
                              errO_.p, ctrl_, f32_, st_);
     else
-        launch_reduce_pairs(k5part_.p, k5_grid(g_), red3_.p, ctrl_, st_);
+        launch_reduce_pairs(k5part_.p, k5n(), red3_.p, ctrl_, st_);
 }
 
 // Single-GPU iteration.  Same kernels and data flow as phases A-D, but each
@@ -691,9 +691,9 @@ void Session::iterate_fused(int k) {
         // all-reduce carries K5(k-1)'s norm partials; the finish of k-1
         // follows it, and every kernel after that checks its stop flag.
         const bool pend = norms_pending_;
-        allreduce(red1_.p, red1_count() + (pend ? 2 * (int64_t)k5_grid(g_) : 0));
+        allreduce(red1_.p, red1_count() + (pend ? 2 * (int64_t)k5n() : 0));
         if (pend) {
-            launch_reduce_finish(red1_.p + red1_count(), k5_grid(g_), normD_, pend_k_, o_.tol,
+            launch_reduce_finish(red1_.p + red1_count(), k5n(), normD_, pend_k_, o_.tol,
                                  errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_);
             norms_pending_ = false;
         }

@@ -106,6 +106,8 @@ class Session {
     // communicator the same order with its three all-reduces
     void iterate_fused(int k);
     bool fused_ = false;
+    // K5's norm-partial count (its workgroups; the fp32 rank-split K5 has more)
+    int k5n() const { return f32_ ? k5_parts32(g_) : k5_grid(g_); }
     int k2side_ = 1;  // update_C's solve beside K2 (0: after it, experiments)
     SideSolve k5side_;  // the side solve of the next K5 launch
     // communicator: K5's norm partials of iteration pend_k_ wait in red1_'s
