@@ -92,6 +92,9 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_PROF
 #define K5_PROF 0  // timing experiments only: s_memtime phase profile of the t-walk (tools/k5_prof.py)
 #endif
+#ifndef K5_BUF
+#define K5_BUF 1  // streams and compact-E slots through wave-based buffer descriptors (see load; interleaved A/B: K5 -0.6 to -1.0 %)
+#endif
 #ifndef K5_WPE
 #define K5_WPE 2  // waves per SIMD at RP <= 64 (one wave: 1.243 vs 0.998 ms, round 3)
 #endif
@@ -221,9 +224,18 @@ __device__ __forceinline__ bool ce_decode_m(double sv, int lane, const uint64_t 
 // wave's 96-double LDS scratch (slot image + a junk area for the zeros).
 // Branch-free: a branch here makes the compiler's vmcnt waits drain the
 // prefetch.
+__device__ __forceinline__ void ce_encode_r(const double (&En)[4], int lane, double* cs,
+                                            __amdgpu_buffer_rsrc_t rs, int soff, d2v* E2, int64_t o,
+                                            unsigned& ndense);
 __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, double* cs, double* CE,
                                           int64_t sb, d2v* E2, int64_t o,
                                           unsigned& ndense) {
+    ce_encode_r(En, lane, cs, wave_rsrc(CE + sb, CE_SLOT * 8), 0, E2, o, ndense);
+}
+// the same with the slot's buffer descriptor and scalar offset given
+__device__ __forceinline__ void ce_encode_r(const double (&En)[4], int lane, double* cs,
+                                            __amdgpu_buffer_rsrc_t rs, int soff, d2v* E2, int64_t o,
+                                            unsigned& ndense) {
     uint64_t nz[4];
     int cnt = 0;
 #pragma unroll
@@ -262,10 +274,9 @@ __device__ __forceinline__ void ce_encode(const double (&En)[4], int lane, doubl
         ++ndense;  // wave-uniform; one atomic per wave at the end (a per-tile
                    // atomic on one counter serialised: 17 -> 53 ms once E turned dense)
     }
-    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(CE + sb, CE_SLOT * 8);
     const double sv = (dense && l >= 4) ? 0.0 : v;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, sv), rs, lane < 32 ? l * 8 : OOB,
-                                          0, 0);
+                                          soff, 0);
 }
 
 // Two waves per SIMD (VGPRs + AGPRs <= 256): at one wave per SIMD the
@@ -434,10 +445,38 @@ void k5_fused(K5Args a) {
         sizeof(double) * (NB * RP * SK + NB * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
                           2 * K5_WAVES + (K5_KRLDS ? K5_WAVES * KS * 64 : 0));
     static_assert(LDS_BYTES <= 160 * 1024, "k5_fused: LDS over the 160 KiB of a CU");
+#if K5_BUF
+    // D, Y_L, T through buffer descriptors based at this wave's first tile:
+    // the t-tile offset is a scalar (soffset), the lane offset a constant
+    // VGPR, so the streams need no per-step 64-bit address VALU
+    // (tm_tile_base = wave base + tt * 1024 doubles)
+    const int64_t wbase = tm_tile_base(tile, 0, ntt);
+    const int wbytes = (int)(ntt * 8192);
+    const __amdgpu_buffer_rsrc_t rD = wave_rsrc(a.D + wbase, wbytes);
+    const __amdgpu_buffer_rsrc_t rYL = wave_rsrc(a.YL + wbase, wbytes);
+    const __amdgpu_buffer_rsrc_t rT = wave_rsrc(a.T + wbase, wbytes);
+    const int vlane = lane * 16;
+    constexpr int BAUX = K5_NT ? 2 : 0;  // nontemporal
+    auto bld = [&](__amdgpu_buffer_rsrc_t r, int64_t tt, int p) {
+        return __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(
+                                            r, vlane + 1024 * p, (int)(phys(tt) * 8192), BAUX));
+    };
+    auto bst = [&](d2v v, __amdgpu_buffer_rsrc_t r, int64_t tt, int p) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, vlane + 1024 * p,
+                                               (int)(phys(tt) * 8192), BAUX);
+    };
+#endif
     auto load = [&](int64_t tt, Regs& nx) {
         const int64_t o = (tm_tile_base(tile, phys(tt), ntt) >> 1) + lane;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
+#if K5_BUF
+            if (!PRO && DY) {
+                nx.x[0][p] = bld(rD, tt, p);
+                nx.x[1][p] = bld(rYL, tt, p);
+                continue;
+            }
+#endif
             nx.x[0][p] = ld2(D2 + o + 64 * p);
             nx.x[1][p] = ld2(YL2 + o + 64 * p);
             if (PRO || !DY) nx.x[2][p] = ld2((PRO ? O2 : YO2) + o + 64 * p);
@@ -453,8 +492,23 @@ void k5_fused(K5Args a) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) nx.edp[p] = Ep2[o + 64 * p];
     };
+#if K5_BUF
+    // compact-E slots: 4 slots (1 KB) per t-tile from the wave's first one
+    const int64_t wslot = (tm_tile_base(tile, 0, ntt) >> 8) * CE_SLOT;
+    const __amdgpu_buffer_rsrc_t rCE = wave_rsrc(a.CE + wslot, (int)(ntt * 1024));
+    const __amdgpu_buffer_rsrc_t rCEp = wave_rsrc(a.CEp + wslot, (int)(ntt * 1024));
+    const int vslot = (lane & 31) * 8;
+#endif
     auto load_slot = [&](int64_t tt, Regs& rx) {
         const int64_t t2 = tt < ntt ? tt : ntt - 1;  // clamped: no branch
+#if K5_BUF
+        if (!PRO) {
+            const int so = (int)(phys(t2) * 1024);
+            rx.ce = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rCE, vslot, so, 0));
+            if (DY) rx.cep = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rCEp, vslot, so, 0));
+            return;
+        }
+#endif
         const int64_t so = (tm_tile_base(tile, phys(t2), ntt) >> 8) * CE_SLOT + (lane & 31);
         rx.ce = a.CE[so];
         if (DY) rx.cep = a.CEp[so];
@@ -689,11 +743,19 @@ void k5_fused(K5Args a) {
                     YOn2[q] = YOn;
                     tr[r] = Tn;
                 }
+#if K5_BUF
+                if (DY) bst(YLn2, rYL, tt, p);
+                else
+#endif
                 st2(YLn2, YL2 + o + 64 * p);
                 if (!DY) st2(YOn2, YO2 + o + 64 * p);
             }
             K5_PT(4);
+#if K5_BUF
+            ce_encode_r(En, lane, cs, DY ? rCEp : rCE, (int)(phys(tt) * 1024), Eout2, o, ndense);
+#else
             ce_encode(En, lane, cs, CEout, (tb >> 8) * CE_SLOT, Eout2, o, ndense);
+#endif
             K5_PT(5);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
@@ -710,6 +772,10 @@ void k5_fused(K5Args a) {
             d2v tv;
             tv[0] = ts[il * 17 + 4 * (2 * p) + tg];
             tv[1] = ts[il * 17 + 4 * (2 * p + 1) + tg];
+#if K5_BUF
+            if (!PRO && DY) bst(tv, rT, tt, p);
+            else
+#endif
             st2(tv, T2 + o + 64 * p);
         }
         }
