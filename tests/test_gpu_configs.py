@@ -225,8 +225,9 @@ def test_config4_recovers_low_rank(tritd, big):
 
 
 def test_config4_pool_probe_does_not_change_results(tritd, big, monkeypatch):
-    """Placement probing picks one of several candidate pools; addresses never
-    enter the arithmetic, so every choice gives bitwise the same iterates."""
+    """Placement probing picks one of several candidate pools (in rounds until a
+    clearly fast one turns up); addresses never enter the arithmetic, so every
+    choice gives bitwise the same iterates."""
     from tritd import synth
     opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
     n = 512
@@ -236,8 +237,13 @@ def test_config4_pool_probe_does_not_change_results(tritd, big, monkeypatch):
         s = tritd.Session(8, opts, big["A0"], big["B0"], big["C0"], n1=n, n2=n, n3=n,
                           D=big["D"], device=0)
         ms, picked = s.probe()
-        assert len(ms) == int(probe) and 0 <= picked < len(ms)
+        # rounds of TRITD_PROBE candidates (up to TRITD_PROBE_ROUNDS = 3) until
+        # one is clearly in the fast placement class; the fastest is kept
+        p = int(probe)
+        assert (len(ms) == 1 if p == 1 else (len(ms) % p == 0 and p <= len(ms) <= 3 * p))
+        assert 0 <= picked < len(ms)
         assert all(m > 0 for m in ms) if len(ms) > 1 else True
+        assert len(ms) == 1 or ms[picked] == min(ms)
         s.run(3)
         out.append(s.get())
         s.close()

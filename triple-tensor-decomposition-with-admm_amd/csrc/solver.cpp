@@ -11,6 +11,7 @@
 // several sessions on one device instead.
 #include "solver.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -543,57 +544,85 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     const char* pe = std::getenv("TRITD_PROBE");
     int want = pe ? std::atoi(pe) : 8;
     if (pool_bytes < ((size_t)1 << 30)) want = 1;
-    size_t fr = 0, tot = 0;
-    TRITD_HIP(hipMemGetInfo(&fr, &tot));
+    // rounds of `want` candidates until both placement classes have shown up
+    // (fastest below 0.92 x slowest: the classes differ by ~10 %), so the one
+    // kept is a fast one; a box whose first eight all landed in one class
+    // (bench line 707 it/s with eight slow pools, vs 730-737) gets up to two
+    // more rounds.  Earlier rounds stay allocated while the next one is
+    // drawn, so it gets new pages.
+    const char* pr = std::getenv("TRITD_PROBE_ROUNDS");
+    const int rounds = pr ? std::atoi(pr) : 3;
     // keep room for the chosen pool, the other session buffers and 4 GiB
     const size_t reserve = pool_bytes / 2 + ((size_t)4 << 30);
-    const size_t room = fr > reserve ? (fr - reserve) / pool_bytes : 0;
-    if ((size_t)want > room) want = room > 1 ? (int)room : 1;
     std::vector<double*> cand;
-    // (hipDeviceMallocContiguous pools probe no differently: tools/contig_probe.py)
-    for (int c = 0; c < want; ++c) {
-        void* p = nullptr;
-        if (hipMalloc(&p, pool_bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            break;
+    auto alloc_round = [&](int n) {
+        size_t fr = 0, tot = 0;
+        TRITD_HIP(hipMemGetInfo(&fr, &tot));
+        const size_t room = fr > reserve ? (fr - reserve) / pool_bytes : 0;
+        if ((size_t)n > room) n = (int)room;
+        if (cand.empty() && n < 1) n = 1;  // the pool itself
+        // (hipDeviceMallocContiguous pools probe no differently: tools/contig_probe.py)
+        for (int c = 0; c < n; ++c) {
+            void* p = nullptr;
+            if (hipMalloc(&p, pool_bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                break;
+            }
+            cand.push_back(static_cast<double*>(p));
         }
-        cand.push_back(static_cast<double*>(p));
-    }
+    };
+    alloc_round(want);
     if (cand.empty()) throw Error(TRITD_ERR_NOMEM, "hipMalloc of the tensor pool failed");
-    probe_ms_.assign(cand.size(), 0.0);
+    probe_ms_.clear();
     size_t best = 0;
-    if (cand.size() > 1) {
+    if (want > 1 && cand.size() > 1) {
         hipEvent_t e0, e1;
         TRITD_HIP(hipEventCreate(&e0));
         TRITD_HIP(hipEventCreate(&e1));
-        for (size_t c = 0; c < cand.size(); ++c) {
-            char* f[6];
-            for (int q = 0; q < 6; ++q) f[q] = reinterpret_cast<char*>(cand[c]) + q * slot + q * stagger;
-            // pool order: D, O, E, YL, YO, T
-            auto probe = [&] {
-                if (f32_)
-                    launch_pool_probe32(g_, (float*)f[0], (float*)f[3], (float*)f[4], (float*)f[5],
-                                        CE_.f(), st_);
-                else
-                    launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[4],
-                                      (double*)f[5], CE_.p, dy_, st_);
-            };
-            probe();  // warm
-            float ms = 1e30f;
-            for (int r = 0; r < 2; ++r) {
-                TRITD_HIP(hipEventRecord(e0, st_));
-                probe();
-                TRITD_HIP(hipEventRecord(e1, st_));
-                TRITD_HIP(hipEventSynchronize(e1));
-                float x = 0.f;
-                TRITD_HIP(hipEventElapsedTime(&x, e0, e1));
-                ms = std::fmin(ms, x);
+        auto probe_from = [&](size_t from) {
+            for (size_t c = from; c < cand.size(); ++c) {
+                char* f[6];
+                for (int q = 0; q < 6; ++q) f[q] = reinterpret_cast<char*>(cand[c]) + q * slot + q * stagger;
+                // pool order: D, O, E, YL, YO, T
+                auto probe = [&] {
+                    if (f32_)
+                        launch_pool_probe32(g_, (float*)f[0], (float*)f[3], (float*)f[4], (float*)f[5],
+                                            CE_.f(), st_);
+                    else
+                        launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[4],
+                                          (double*)f[5], CE_.p, dy_, st_);
+                };
+                probe();  // warm
+                float ms = 1e30f;
+                for (int r = 0; r < 2; ++r) {
+                    TRITD_HIP(hipEventRecord(e0, st_));
+                    probe();
+                    TRITD_HIP(hipEventRecord(e1, st_));
+                    TRITD_HIP(hipEventSynchronize(e1));
+                    float x = 0.f;
+                    TRITD_HIP(hipEventElapsedTime(&x, e0, e1));
+                    ms = std::fmin(ms, x);
+                }
+                probe_ms_.push_back(ms);
+                if (ms < probe_ms_[best]) best = c;
             }
-            probe_ms_[c] = ms;
-            if (ms < probe_ms_[best]) best = c;
+        };
+        // both placement classes seen: the fastest candidate is a fast one
+        auto clearly_fast = [&] {
+            const auto mm = std::minmax_element(probe_ms_.begin(), probe_ms_.end());
+            return *mm.first < 0.92 * *mm.second;
+        };
+        probe_from(0);
+        for (int r = 1; r < rounds && !clearly_fast(); ++r) {
+            const size_t from = cand.size();
+            alloc_round(want);
+            if (cand.size() == from) break;
+            probe_from(from);
         }
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+    } else {
+        probe_ms_.assign(cand.size(), 0.0);
     }
     for (size_t c = 0; c < cand.size(); ++c)
         if (c != best) (void)hipFree(cand[c]);

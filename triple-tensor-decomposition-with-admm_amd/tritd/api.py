@@ -455,10 +455,11 @@ class Session:
 
     def probe(self):
         """(probe ms of each candidate tensor pool, index kept)"""
-        ms = (C.c_double * 16)()
+        cap = 64  # up to three rounds of candidates (solver.cpp probe_pool)
+        ms = (C.c_double * cap)()
         n, k = _lib.i32(0), _lib.i32(0)
-        check(lib.tritd_session_probe(self._s, ms, 16, C.byref(n), C.byref(k)))
-        return [ms[i] for i in range(min(n.value, 16))], k.value
+        check(lib.tritd_session_probe(self._s, ms, cap, C.byref(n), C.byref(k)))
+        return [ms[i] for i in range(min(n.value, cap))], k.value
 
     def counters(self):
         """(E tiles stored densely over all fused-update launches, tiles per launch)"""
