@@ -348,12 +348,22 @@ void k5_fused(K5Args a) {
     constexpr int SP = 16 * RP / 2;                 // (v0,v1) pairs per slice
     constexpr int NS = (SP + 64 * K5_WAVES - 1) / (64 * K5_WAVES);
     d2v sv[NS];
+#if K5_BUF
+    // C^ slices through one descriptor: slice tt at a scalar offset
+    const __amdgpu_buffer_rsrc_t rCh = wave_rsrc(a.Ch, (int)(a.n3p * RP * 8));
+#endif
     auto stage_load = [&](int64_t tt) {
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int e = threadIdx.x + q * 64 * K5_WAVES;
-            if (SP % (64 * K5_WAVES) == 0 || e < SP)
+            if (SP % (64 * K5_WAVES) == 0 || e < SP) {
+#if K5_BUF
+                sv[q] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rCh, 16 * e, (int)(phys(tt) * 16 * RP * 8), 0));
+#else
                 sv[q] = *reinterpret_cast<const d2v*>(a.Ch + (phys(tt) << 4) * RP + 2 * e);
+#endif
+            }
         }
     };
     auto stage_store = [&](int buf) {
