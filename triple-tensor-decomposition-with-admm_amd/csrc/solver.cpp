@@ -547,11 +547,13 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     // rounds of `want` candidates until both placement classes have shown up
     // (fastest below 0.92 x slowest: the classes differ by ~10 %), so the one
     // kept is a fast one; a box whose first eight all landed in one class
-    // (bench line 707 it/s with eight slow pools, vs 730-737) gets up to two
-    // more rounds.  Earlier rounds stay allocated while the next one is
-    // drawn, so it gets new pages.
+    // (bench line 707 it/s with eight slow pools, vs 730-737) gets one more
+    // round (a second one-class round is taken as that box's only class: with
+    // one third of the pools fast, sixteen slow ones in a row are rare).
+    // Earlier rounds stay allocated while the next one is drawn, so it gets
+    // new pages.
     const char* pr = std::getenv("TRITD_PROBE_ROUNDS");
-    const int rounds = pr ? std::atoi(pr) : 3;
+    const int rounds = pr ? std::atoi(pr) : 2;
     // keep room for the chosen pool, the other session buffers and 4 GiB
     const size_t reserve = pool_bytes / 2 + ((size_t)4 << 30);
     std::vector<double*> cand;
