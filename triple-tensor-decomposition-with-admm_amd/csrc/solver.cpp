@@ -543,7 +543,9 @@ void Session::phaseC(int k) {
 double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     const char* pe = std::getenv("TRITD_PROBE");
     int want = pe ? std::atoi(pe) : 8;
-    if (pool_bytes < ((size_t)1 << 30)) want = 1;
+    // (small pools too: a mode-1 shard of 64 rows at 512^3 is a 0.8 GB pool, and
+    // the slowest of P ranks sets the sharded iteration)
+    if (pool_bytes < ((size_t)128 << 20)) want = 1;
     // rounds of `want` candidates until both placement classes have shown up
     // (fastest below 0.92 x slowest: the classes differ by ~10 %), so the one
     // kept is a fast one; a box whose first eight all landed in one class
