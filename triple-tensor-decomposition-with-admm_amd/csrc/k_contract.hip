@@ -632,13 +632,17 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
 // factors A^TA, B^TB, C^TC of update_A/B/C (:77,86,93 build F F^T etc.;
 // SURVEY.md §0.3).  One workgroup per 16 x 16 tile of G: the rows go to
 // v_mfma_f64_16x16x4_f64 four at a time (A[m][k] = X(i0+k, 16ta+m),
-// B[k][n] = X(i0+k, 16tb+n)), the 4 waves take every 4th K-step and are
+// B[k][n] = X(i0+k, 16tb+n)), the NW waves take every NW-th K-step and are
 // summed through LDS in fixed order (deterministic).  Out-of-range rows load
 // as zero.  Latency-bound at these sizes; the old per-column VALU loop took
 // 29 us at 512 x 64, this takes a few.
-__global__ __launch_bounds__(256) void k_gram(const double* __restrict__ X, int64_t rows, int RP,
-                                              double* G, const int* stop) {
+// NW waves per workgroup (16: every wave's K-steps in flight at once — 512
+// rows are 128 K-steps, 8 per wave, one load round instead of eight).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_gram(const double* __restrict__ X, int64_t rows, int RP,
+                                                  double* G, const int* stop) {
     if (stop && *stop) return;
+    constexpr int U = 8;  // K-steps per wave per round: loads first
     const int nt = RP >> 4;
     const int ta = blockIdx.x / nt, tb = blockIdx.x - (blockIdx.x / nt) * nt;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -647,28 +651,30 @@ __global__ __launch_bounds__(256) void k_gram(const double* __restrict__ X, int6
     const double* xb = X + 16 * tb + m;
     const int64_t steps = (rows + 3) >> 2;
     d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-    for (int64_t s = w; s < steps; s += 16) {  // K-steps s, s+4, s+8, s+12: loads first
-        double a[4], b[4];
+    for (int64_t s = w; s < steps; s += U * NW) {  // K-steps s, s+NW, ..., s+(U-1)NW
+        double a[U], b[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t i = 4 * (s + 4 * u) + kq;
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = 4 * (s + NW * u) + kq;
             const bool in = i < rows;
             a[u] = in ? xa[i * RP] : 0.0;
             b[u] = in ? xb[i * RP] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc = mfma4(a[u], b[u], acc);
+        for (int u = 0; u < U; ++u) acc = mfma4(a[u], b[u], acc);
     }
-    __shared__ double part[3][4][64];
+    __shared__ double part[NW - 1][4][64];
     if (w > 0)
 #pragma unroll
         for (int r = 0; r < 4; ++r) part[w - 1][r][lane] = acc[r];
     __syncthreads();
     if (w == 0) {
-        // C/D element r of lane l: G(16ta + (l>>4) + 4r, 16tb + (l&15))
+        // C/D element r of lane l: G(16ta + (l>>4) + 4r, 16tb + (l&15)); waves summed in order
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const double v = ((acc[r] + part[0][r][lane]) + part[1][r][lane]) + part[2][r][lane];
+            double v = acc[r];
+#pragma unroll
+            for (int q = 0; q < NW - 1; ++q) v += part[q][r][lane];
             G[(int64_t)(16 * ta + kq + 4 * r) * RP + 16 * tb + m] = v;
         }
     }
@@ -676,7 +682,10 @@ __global__ __launch_bounds__(256) void k_gram(const double* __restrict__ X, int6
 
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_gram, dim3((RP / 16) * (RP / 16)), dim3(256), 0, st, X, rows, RP, G, stop);
+#ifndef TRITD_GRAM_NW
+#define TRITD_GRAM_NW 16
+#endif
+    hipLaunchKernelGGL(k_gram<TRITD_GRAM_NW>, dim3((RP / 16) * (RP / 16)), dim3(64 * TRITD_GRAM_NW), 0, st, X, rows, RP, G, stop);
     TRITD_CHECK_LAUNCH();
 }
 
