@@ -495,8 +495,18 @@ __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ pa
     const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
     const int64_t e = (int64_t)blockIdx.x * 64 + lane;
     double s = 0.0;
-    if (e < count)
+    if (nparts <= 4 * 16) {  // (512^3: 64 parts) every load issued before the in-order sum
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int y = q + 4 * u;
+            v[u] = (e < count && y < nparts) ? part[(int64_t)y * count + e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+    } else if (e < count) {
         for (int y = q; y < nparts; y += 4) s += part[(int64_t)y * count + e];
+    }
     __shared__ double red[4][64];
     red[q][lane] = s;
     __syncthreads();
