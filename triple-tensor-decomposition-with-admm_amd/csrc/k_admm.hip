@@ -421,7 +421,7 @@ void k5_fused(K5Args a) {
     d2v* E2 = reinterpret_cast<d2v*>(a.E);
     d2v* Ep2 = reinterpret_cast<d2v*>(a.Ep);     // DY: E^(k-1) dense tiles, E^(k+1) destination
     d2v* Eout2 = DY ? Ep2 : E2;
-    double* CEout = DY ? a.CEp : a.CE;
+    [[maybe_unused]] double* CEout = DY ? a.CEp : a.CE;
     d2v* YL2 = reinterpret_cast<d2v*>(a.YL);
     d2v* YO2 = reinterpret_cast<d2v*>(a.YO);
     d2v* T2 = reinterpret_cast<d2v*>(a.T);

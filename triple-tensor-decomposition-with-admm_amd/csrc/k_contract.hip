@@ -151,23 +151,29 @@ void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, co
 // side: workgroup 0 runs update_B's R x R solve (sweep.h) beside the
 // contraction (one GPU: its A^TA needs no all-reduce); the grid is 1-D,
 // workgroup b >= side.on takes (j, k-group) = ((b - on) % n2, (b - on) / n2)
-template <int RP>
-__global__ __launch_bounds__(256) void k_m2(const double* __restrict__ Wk,
-                                            const double* __restrict__ AhT, double* M2,
-                                            int64_t n1p, int64_t n2, int64_t plane,
-                                            const int* stop, SideSolve side) {
+// NWV waves per workgroup: 8, so the side solve's sweep runs 8 rows per
+// lane (its barrier-bound pivot steps are the part of M2 + solve that
+// outlasts the contraction)
+#ifndef TRITD_M2_NW
+#define TRITD_M2_NW 8
+#endif
+template <int RP, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_m2(const double* __restrict__ Wk,
+                                                 const double* __restrict__ AhT, double* M2,
+                                                 int64_t n1p, int64_t n2, int64_t plane,
+                                                 const int* stop, SideSolve side) {
     if (*stop) return;
-    if constexpr (RP <= 64) {
+    if constexpr (RP <= 64 && RP % NWV == 0) {
         if (side.on && blockIdx.x == 0) {
-            __shared__ double srow[2 * 4 * 64 + RP];
-            side_solve<RP>(side, srow, srow + 2 * 4 * 64);
+            __shared__ double srow[2 * NWV * 64 + RP];
+            side_solve<RP, NWV>(side, srow, srow + 2 * NWV * 64);
             return;
         }
     }
     const int64_t b = (int64_t)blockIdx.x - side.on;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t j = b % n2;
-    const int k = (int)(b / n2) * 4 + w;
+    const int k = (int)(b / n2) * NWV + w;
     if (k >= RP) return;
     // 16-B loads (n1p % 16 == 0): lane sums rows 2l, 2l+1, 2l+128, ... in two chains
     const d2v* wp = reinterpret_cast<const d2v*>(Wk + (int64_t)k * plane + j * n1p);
@@ -187,14 +193,15 @@ __global__ __launch_bounds__(256) void k_m2(const double* __restrict__ Wk,
 void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, const int* stop,
                hipStream_t st, const SideSolve& side) {
     if (side.on && g.RP > 64) throw Error(TRITD_ERR_ARG, "M2 side solve: RP <= 64 only");
-    const dim3 grid((unsigned)(g.n2 * cdiv(g.RP, 4) + side.on));
+    constexpr int NV = TRITD_M2_NW;
+    const dim3 grid((unsigned)(g.n2 * cdiv(g.RP, NV) + side.on)), blk(64 * NV);
     switch (g.RP) {
-        case 16: hipLaunchKernelGGL(k_m2<16>, grid, dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 32: hipLaunchKernelGGL(k_m2<32>, grid, dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 48: hipLaunchKernelGGL(k_m2<48>, grid, dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 64: hipLaunchKernelGGL(k_m2<64>, grid, dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 128: hipLaunchKernelGGL(k_m2<128>, grid, dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 256: hipLaunchKernelGGL(k_m2<256>, grid, dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        case 16: hipLaunchKernelGGL((k_m2<16, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        case 32: hipLaunchKernelGGL((k_m2<32, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        case 48: hipLaunchKernelGGL((k_m2<48, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        case 64: hipLaunchKernelGGL((k_m2<64, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        case 128: hipLaunchKernelGGL((k_m2<128, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        case 256: hipLaunchKernelGGL((k_m2<256, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
         default: throw Error(TRITD_ERR_UNSUPPORTED, "M2: RP not supported");
     }
     TRITD_CHECK_LAUNCH();

@@ -53,16 +53,17 @@ __device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, doubl
     (sweep_step<RP, RW, Ps>(a, rowbuf, pivs, c, w), ...);
 }
 
-// inv(P o Q + alpha I) by the sweep in one 256-thread workgroup: 4 waves of
-// RP/4 rows per lane, lane = column (k_solve's algorithm and rounding with
-// another row split).  rowbuf: 2*4*64 doubles, pivs: RP doubles of LDS.
+// inv(P o Q + alpha I) by the sweep in one workgroup of NW waves (the host
+// kernel's block): RP/NW rows per lane, lane = column (k_solve's algorithm
+// and rounding with another row split).  rowbuf: 2*NW*64 doubles, pivs: RP
+// doubles of LDS.
 // Ginv is written directly (R x R block, zero pad); the pinv-tolerance check
 // of k_solve raises flags[0].
-template <int RP>
+template <int RP, int NW = 4>
 __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, double* pivs) {
     // the host kernel's other workgroups share this CU's SIMDs: win issue
     __builtin_amdgcn_s_setprio(3);
-    constexpr int NW = 4, RW = RP / NW;
+    constexpr int RW = RP / NW;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int cc = c < RP ? c : 0;  // lanes >= RP read a valid column, never written back
     double a[RW];
