@@ -1,6 +1,6 @@
 """Dev helper: K5 / K2 time of a mode-1 shard of the config-4 problem as a
 function of its row count (a shard of rows [0, i1), one-rank RCCL schedule).
-usage: python tools/rows_sweep.py i1 [i1 ...]"""
+usage: [ROWS_SKIP=10] python tools/rows_sweep.py i1 [i1 ...]"""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,11 +18,13 @@ for i1 in [int(x) for x in sys.argv[1:]]:
     comm = tritd.Comm(tritd.Comm.unique_id(), 1, 0, 0)
     s = tritd.Session(r, opts, d["A0"], d["B0"], d["C0"], n1=n, n2=n, n3=n, i0=0, i1=i1,
                       D=np.asfortranarray(d["D"][:i1]), device=0, comm=comm)
-    s.run(10); s.sync()
+    s.run(int(os.environ.get("ROWS_SKIP", "10"))); s.sync()
+    d0, tpl = s.counters()
     s.set_timing(True); s.run(40); s.sync()
+    d1, _ = s.counters()
     km = s.kernel_ms()
-    print("rows=%d iteration %.4f ms  k5 %.4f (%.4f per 512 rows)  m3 %.4f  probe %s" %
+    print("rows=%d iteration %.4f ms  k5 %.4f (%.4f per 512 rows)  m3 %.4f  dense E tiles %.4f %%  probe %s" %
           (i1, km["iteration"], km["fused_update"], km["fused_update"] * 512 / i1, km["mode3"],
-           s.probe()), flush=True)
+           100.0 * (d1 - d0) / 40 / tpl, s.probe()), flush=True)
     s.close()
     comm.close()
