@@ -50,7 +50,7 @@ AlsSession::AlsSession(int device, const double* X, int64_t ldX, int64_t n1, int
     // one inverse per Gram slot, kept across iterations (k_solve_ns refines
     // the previous one); zero = no start
     for (DBuf* b : {&GinvA_, &GinvB_, &GinvC_}) {
-        b->alloc((size_t)g_.RP * g_.RP);
+        b->alloc(ginv_count(g_.RP));  // inverse + pinv fallback space (pinv.h)
         TRITD_HIP(hipMemsetAsync(b->p, 0, b->bytes(), st_));
     }
     BtB_.alloc((size_t)g_.RP * g_.RP);
@@ -189,7 +189,7 @@ void AlsSession::phaseA(int k) {
     launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
     // ALS :27 ridge 1e-9; test.m:82 ridge 1e-12, then the reweighted shrink :86-89
     launch_solve(RP, g_.R, BtB_.p, CtC_.p, ncvx_ ? 1e-12 : 1e-9, GinvA_.p, ctrl_ + 2, ctrl_, st_);
-    launch_apply(RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+    launch_apply(RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, ctrl_, ctrl_ + 2, st_);
     if (ncvx_)
         launch_ncvx_shrink(g_, Ah_.p, AhT_.p, np_.gamma_A, np_.epsilon, np_.theta - np_.p, ctrl_,
                            st_);
@@ -203,7 +203,7 @@ void AlsSession::phaseB(int k) {
     const double* M2 = red1_.p;
     const double* AtA = red1_.p + g_.n2 * RP;
     launch_solve(RP, g_.R, AtA, CtC_.p, 1e-9, GinvB_.p, ctrl_ + 2, ctrl_, st_);  // :32
-    launch_apply(RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, ctrl_, st_);
+    launch_apply(RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, ctrl_, ctrl_ + 2, st_);
     launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     if (timing_) TRITD_HIP(hipEventRecord(ev_[ev_.size() - 3], st_));
     launch_m3(g_, XT_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_);
@@ -215,7 +215,7 @@ void AlsSession::phaseC(int k) {
     const int RP = g_.RP;
     const double* AtA = red1_.p + g_.n2 * RP;
     launch_solve(RP, g_.R, AtA, BtB_.p, 1e-9, GinvC_.p, ctrl_ + 2, ctrl_, st_);  // :37
-    launch_apply(RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+    launch_apply(RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, ctrl_, ctrl_ + 2, st_);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
 }
 

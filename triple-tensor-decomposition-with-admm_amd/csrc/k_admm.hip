@@ -1002,10 +1002,14 @@ __global__ void k_finish(const double* ss, double normD, int k, double tol, doub
     finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl, single);
 }
 
-__global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict__ p, int n,
+// clear: zero the pairs after reading them (each thread clears the pairs it
+// read).  The sharded schedule's norm partials live in red1_'s tail, sized to
+// the largest shard's K5 grid; a rank with fewer workgroups leaves the slots
+// past its own at zero, and the all-reduce writes sums into all of them.
+__global__ __launch_bounds__(256) void k_reduce_finish(double* __restrict__ p, int n,
                                                        double normD, int k, double tol,
                                                        double* errHist, double* errL, double* errO,
-                                                       int* ctrl, int single) {
+                                                       int* ctrl, int single, int clear) {
     if (ctrl[0]) return;
     __shared__ double sx[256], sy[256];
     double x = 0.0, y = 0.0;
@@ -1014,6 +1018,11 @@ __global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict_
         x += p[2 * b];
         y += p[2 * b + 1];
     }
+    if (clear)
+        for (int b = threadIdx.x; b < n; b += 256) {
+            p[2 * b] = 0.0;
+            p[2 * b + 1] = 0.0;
+        }
     sx[threadIdx.x] = x;
     sy[threadIdx.x] = y;
     __syncthreads();
@@ -1030,11 +1039,11 @@ __global__ __launch_bounds__(256) void k_reduce_finish(const double* __restrict_
     }
 }
 
-void launch_reduce_finish(const double* partial, int n, double normD, int k, double tol,
+void launch_reduce_finish(double* partial, int n, double normD, int k, double tol,
                           double* errHist, double* errL, double* errO, int* ctrl, bool single,
-                          hipStream_t st) {
+                          hipStream_t st, bool clear) {
     hipLaunchKernelGGL(k_reduce_finish, dim3(1), dim3(256), 0, st, partial, n, normD, k, tol,
-                       errHist, errL, errO, ctrl, (int)single);
+                       errHist, errL, errO, ctrl, (int)single, (int)clear);
     TRITD_CHECK_LAUNCH();
 }
 

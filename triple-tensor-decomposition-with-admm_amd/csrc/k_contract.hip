@@ -192,8 +192,12 @@ __global__ __launch_bounds__(64 * NWV) void k_m2(const double* __restrict__ Wk,
 
 void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, const int* stop,
                hipStream_t st, const SideSolve& side) {
-    if (side.on && g.RP > 64) throw Error(TRITD_ERR_ARG, "M2 side solve: RP <= 64 only");
     constexpr int NV = TRITD_M2_NW;
+    static_assert(NV >= 1 && NV <= 16, "TRITD_M2_NW: 1..16 waves per workgroup");
+    // k_m2 instantiates the side solve only where RP % NV == 0; anywhere else
+    // workgroup 0 would fall through to the contraction with b = -1
+    if (side.on && (g.RP > 64 || g.RP % NV != 0))
+        throw Error(TRITD_ERR_ARG, "M2 side solve: RP <= 64 and a multiple of TRITD_M2_NW only");
     const dim3 grid((unsigned)(g.n2 * cdiv(g.RP, NV) + side.on)), blk(64 * NV);
     switch (g.RP) {
         case 16: hipLaunchKernelGGL((k_m2<16, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
@@ -720,8 +724,8 @@ void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* st
 // wave publishes its candidate of row P (only the owner's is read), one
 // barrier, double-buffered by step parity (8 rows per lane, RP/8 waves).  The smallest pivot (= smallest
 // LDL^T pivot) is compared with MATLAB's pinv tolerance max(size)*eps(max
-// sigma); flags[0] is raised when pinv could truncate
-// (triple_decomp_ADMM.m:78,86,93 use pinv).
+// sigma); within 1e3x of it, pinv could truncate (triple_decomp_ADMM.m:78,86,93
+// use pinv) and the solve requests the pinv fallback of pinv.h.
 // Register-pressure notes (each measured): the pivot loop is unrolled via an
 // index sequence (a runtime pivot would index the register array); there is
 // no divergent branch and no per-element runtime mask inside or after the
@@ -769,16 +773,7 @@ __global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __
         const int i = e / RP, j = e - (e / RP) * RP;
         Ginv[e] = (i < R && j < R) ? outb[i * 64 + j] : 0.0;
     }
-    if (threadIdx.x == 0) {
-        double minpiv = 1e308, maxpiv = 0.0;
-        for (int p = 0; p < R; ++p) {
-            minpiv = fmin(minpiv, pivs[p]);
-            maxpiv = fmax(maxpiv, pivs[p]);
-        }
-        // eps(x) = 2^(floor(log2 x) - 52)
-        const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);
-        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
-    }
+    pinv_request<NT>(pivots_near_cutoff(pivs, R), P, Q, R, RP, alpha, Ginv);
 }
 
 
@@ -799,10 +794,12 @@ __global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __
 // a zero or stale buffer, a NaN) the kernel runs the sweep instead, so the
 // result is an inverse to working accuracy either way.
 //
-// pinv-tolerance flag (triple_decomp_ADMM.m:78,86,93 use pinv): the sweep
-// path compares its LDL^T pivots as k_solve does; the Newton path uses the
-// bounds sigma_min >= 1/||X||_F and sigma_max <= ||G||_F, i.e. it raises
-// the flag whenever the sweep could (and up to sqrt(R) earlier).
+// pinv fallback request (triple_decomp_ADMM.m:78,86,93 use pinv; pinv.h):
+// the sweep path compares its LDL^T pivots as k_solve does; the Newton path
+// uses the bounds sigma_min >= 1/||X||_F and sigma_max <= ||G||_F, i.e. it
+// requests whenever the sweep could (and up to sqrt(R) earlier).  Either way
+// the fallback computes pinv itself and raises TRITD_FLAG_PINV_TOL only when
+// pinv drops a value, so the flag does not depend on which test asked.
 //
 // Waves: RP/4 (the sweep runs 4 rows per lane); the Newton GEMMs use the
 // first (RP/16)^2 of them.
@@ -924,13 +921,6 @@ __global__ __launch_bounds__(RP * 16) void k_solve_ns(const double* __restrict__
 #pragma unroll
             for (int q = 0; q < RW; ++q) Xs[(RW * w + q) * LD + c] = -a[q];
         __syncthreads();
-        if (tid == 0) {
-            minpiv = 1e308;
-            for (int p = 0; p < R; ++p) {
-                minpiv = fmin(minpiv, pivs[p]);
-                maxpiv = fmax(maxpiv, pivs[p]);
-            }
-        }
     }
     double xss = 0.0;
     for (int e = tid; e < RP * RP; e += NTH) {
@@ -940,7 +930,10 @@ __global__ __launch_bounds__(RP * 16) void k_solve_ns(const double* __restrict__
         Ginv[e] = x;
         xss = fma(x, x, xss);
     }
-    if (!sweep) {
+    bool near;
+    if (sweep) {
+        near = pivots_near_cutoff(pivs, R);
+    } else {
         xss = wave_sum(xss);
         gss = wave_sum(gss);
         if (lane == 0) {
@@ -948,20 +941,17 @@ __global__ __launch_bounds__(RP * 16) void k_solve_ns(const double* __restrict__
             red[1][w] = gss;
         }
         __syncthreads();
-        if (tid == 0) {
-            double x2 = 0.0, g2 = 0.0;
-            for (int q = 0; q < NWV; ++q) {
-                x2 += red[0][q];
-                g2 += red[1][q];
-            }
-            minpiv = 1.0 / sqrt(x2);
-            maxpiv = sqrt(g2);
+        double x2 = 0.0, g2 = 0.0;  // every thread, same order
+        for (int q = 0; q < NWV; ++q) {
+            x2 += red[0][q];
+            g2 += red[1][q];
         }
-    }
-    if (tid == 0) {
+        minpiv = 1.0 / sqrt(x2);
+        maxpiv = sqrt(g2);
         const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);  // pinv: R*eps(sigma_max)
-        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
+        near = !(minpiv > 1e3 * tol);
     }
+    pinv_request<NTH>(near, P, Q, R, RP, alpha, Ginv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1099,15 +1089,7 @@ __global__ __launch_bounds__(1024) void k_solve_big(const double* __restrict__ P
         const int i = r0 + q;
         S[i * RP + c] = (i < R && c < R) ? -S[i * RP + c] : 0.0;
     }
-    if (tid == 0) {
-        double minpiv = 1e308, maxpiv = 0.0;
-        for (int p = 0; p < R; ++p) {
-            minpiv = fmin(minpiv, pivs[p]);
-            maxpiv = fmax(maxpiv, pivs[p]);
-        }
-        const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);
-        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
-    }
+    pinv_request<1024>(pivots_near_cutoff(pivs, R), P, Q, R, RP, alpha, S);
 }
 
 static size_t solve_big_lds(int RP) {
@@ -1255,15 +1237,7 @@ __global__ __launch_bounds__(64 * solve_blk_waves<RP>()) void k_solve_blk(
         const int i = e / RP, j = e - (e / RP) * RP;
         Ginv[e] = (i < R && j < R) ? -S[i * LD + j] : 0.0;
     }
-    if (tid == 0) {
-        double minpiv = 1e308, maxpiv = 0.0;
-        for (int p = 0; p < R; ++p) {
-            minpiv = fmin(minpiv, pivs[p]);
-            maxpiv = fmax(maxpiv, pivs[p]);
-        }
-        const double tol = (double)R * ldexp(1.0, ilogb(maxpiv) - 52);
-        if (!(minpiv > 1e3 * tol)) atomicOr(flags, 1);
-    }
+    pinv_request<NT>(pivots_near_cutoff(pivs, R), P, Q, R, RP, alpha, Ginv);
 }
 
 template <int RP>
@@ -1362,12 +1336,13 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
 template <int RP>
 __global__ __launch_bounds__(64 * (RP / 16)) void k_apply(const double* __restrict__ M, int64_t rows,
                                                            const double* __restrict__ Ginv, double* Y,
-                                                           double* YT, int64_t ldT, const int* stop) {
+                                                           double* YT, int64_t ldT, const int* stop,
+                                                           int* flags) {
     // one wave per 16 x 16 tile of Y: rows r0..r0+15, columns 16*tn..;
     // v_mfma_f64_16x16x4_f64 over the RP/4 K-steps, every operand loaded
     // before the chain (A[m][k] = M(r0+m, 4s+k), B[k][n] = Ginv(4s+k, 16tn+n))
     if (stop && *stop) return;
-    constexpr int KS = RP / 4;
+    constexpr int KS = RP / 4, NT = 64 * (RP / 16), LDP = RP + 1;
     const int lane = threadIdx.x & 63, tn = threadIdx.x >> 6;
     const int m = lane & 15, kq = lane >> 4;
     const int64_t r0 = (int64_t)blockIdx.x * 16;
@@ -1375,10 +1350,29 @@ __global__ __launch_bounds__(64 * (RP / 16)) void k_apply(const double* __restri
     const double* mp = M + (r0 + m) * RP + kq;
     const double* gp = Ginv + (int64_t)kq * RP + 16 * tn + m;
     double a[KS], b[KS];
+    const double req = Ginv[ginv_req(RP)];  // the same word in every thread
+    if (req != 0.0) {
+        // the solve's pivots came near pinv's cutoff: every workgroup forms
+        // pinv(saved Gram) in LDS (pinv.h) and multiplies by it instead
+        __shared__ double pA[RP * LDP], pV[RP * LDP], rot[RP], red[NT / 64 + RP];
+        __shared__ int pq[RP];
+        for (int e = threadIdx.x; e < RP * RP; e += NT) {
+            const int i = e / RP, j = e - (e / RP) * RP;
+            pA[i * LDP + j] = Ginv[(int64_t)RP * RP + e];
+        }
+        __syncthreads();
+        jacobi_pinv<RP, NT>(pA, pV, LDP, (int)req, pA, LDP, rot, pq, red, flags);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        a[s] = in ? mp[4 * s] : 0.0;
-        b[s] = gp[(int64_t)4 * s * RP];
+        for (int s = 0; s < KS; ++s) {
+            a[s] = in ? mp[4 * s] : 0.0;
+            b[s] = pA[(4 * s + kq) * LDP + 16 * tn + m];
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            a[s] = in ? mp[4 * s] : 0.0;
+            b[s] = gp[(int64_t)4 * s * RP];
+        }
     }
     d4 acc = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1395,15 +1389,64 @@ __global__ __launch_bounds__(64 * (RP / 16)) void k_apply(const double* __restri
 }
 
 void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, double* Y, double* YT,
-                  int64_t ldT, const int* stop, hipStream_t st) {
+                  int64_t ldT, const int* stop, int* flags, hipStream_t st) {
     const dim3 grid((unsigned)cdiv(rows, 16)), block(64 * (RP / 16));
+#define APPLY_CASE(RPV) \
+    case RPV: hipLaunchKernelGGL(k_apply<RPV>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop, flags); break;
     switch (RP) {
-        case 16: hipLaunchKernelGGL(k_apply<16>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
-        case 32: hipLaunchKernelGGL(k_apply<32>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
-        case 48: hipLaunchKernelGGL(k_apply<48>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
-        case 64: hipLaunchKernelGGL(k_apply<64>, grid, block, 0, st, M, rows, Ginv, Y, YT, ldT, stop); break;
+        APPLY_CASE(16)
+        APPLY_CASE(32)
+        APPLY_CASE(48)
+        APPLY_CASE(64)
         default: throw Error(TRITD_ERR_UNSUPPORTED, "apply: RP not supported");
     }
+#undef APPLY_CASE
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// The pinv fallback as a launch of its own (before the generic apply of the
+// fp32 path and of RP > 64; pinv.h): one workgroup, returns at once unless
+// the solve set the request word.  RP <= 64 works in LDS; 128 / 256 in the
+// Ginv buffer's scratch (the saved Gram is rotated in place, V beside it).
+// ---------------------------------------------------------------------------
+template <int RP>
+__global__ __launch_bounds__(RP <= 64 ? 256 : 1024) void k_pinv_fix(double* Ginv, const int* stop,
+                                                                    int* flags) {
+    if (*stop) return;
+    const double req = Ginv[ginv_req(RP)];
+    if (req == 0.0) return;
+    constexpr int NT = RP <= 64 ? 256 : 1024;
+    __shared__ double rot[RP], red[NT / 64 + RP];
+    __shared__ int pq[RP];
+    double* G = Ginv + (int64_t)RP * RP;
+    if constexpr (RP <= 64) {
+        constexpr int LDP = RP + 1;
+        __shared__ double pA[RP * LDP], pV[RP * LDP];
+        for (int e = threadIdx.x; e < RP * RP; e += NT) {
+            const int i = e / RP, j = e - (e / RP) * RP;
+            pA[i * LDP + j] = G[e];
+        }
+        __syncthreads();
+        jacobi_pinv<RP, NT>(pA, pV, LDP, (int)req, Ginv, RP, rot, pq, red, flags);
+    } else {
+        jacobi_pinv<RP, NT>(G, G + (int64_t)RP * RP, RP, (int)req, Ginv, RP, rot, pq, red, flags);
+    }
+}
+
+void launch_pinv_fix(int RP, double* Ginv, const int* stop, int* flags, hipStream_t st) {
+#define FIX_CASE(RPV) \
+    case RPV: hipLaunchKernelGGL(k_pinv_fix<RPV>, dim3(1), dim3(RPV <= 64 ? 256 : 1024), 0, st, Ginv, stop, flags); break;
+    switch (RP) {
+        FIX_CASE(16)
+        FIX_CASE(32)
+        FIX_CASE(48)
+        FIX_CASE(64)
+        FIX_CASE(128)
+        FIX_CASE(256)
+        default: throw Error(TRITD_ERR_UNSUPPORTED, "pinv fallback: RP not supported");
+    }
+#undef FIX_CASE
     TRITD_CHECK_LAUNCH();
 }
 

@@ -261,9 +261,10 @@ __global__ __launch_bounds__(256) void k_apply_gen(const TM* __restrict__ M, int
     }
 }
 
-void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, const double* Ginv,
+void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, double* Ginv,
                       double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
-                      hipStream_t st) {
+                      int* flags, hipStream_t st) {
+    launch_pinv_fix(RP, Ginv, stop, flags, st);
     const size_t lds = (size_t)16 * (RP + 1) * sizeof(double);
     const dim3 grid((unsigned)cdiv(rows, 16)), block(256);
     if (Mf)

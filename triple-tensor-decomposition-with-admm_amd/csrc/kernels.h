@@ -71,9 +71,9 @@ void launch_reduce_pairs(const double* partial, int n, double* out, const int* s
 // both in one launch (single GPU: nothing to all-reduce in between)
 // single: D is of class single, so errHist(k) = single(norm/normD + norm/normD)
 // with the norms rounded to single (MATLAB class rules)
-void launch_reduce_finish(const double* partial, int n, double normD, int k, double tol,
+void launch_reduce_finish(double* partial, int n, double normD, int k, double tol,
                           double* errHist, double* errL, double* errO, int* ctrl, bool single,
-                          hipStream_t st);
+                          hipStream_t st, bool clear = false);
 // errHist bookkeeping + stop test (triple_decomp_ADMM.m:59,63)
 void launch_finish(const double* ss, double normD, int k, double tol, double* errHist, double* errL,
                    double* errO, int* ctrl, bool single, hipStream_t st);
@@ -93,12 +93,23 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
                const SideSolve& side = SideSolve{});
 // G = X^T X over `rows` rows of a row-major [rows][RP] factor
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop, hipStream_t st);
-// Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere)
+// Ginv buffers, one per Gram slot (pinv.h): [0, RP^2) the inverse, read by
+// the apply; [RP^2, 2 RP^2) the Gram, saved by a solve whose pivot test came
+// near pinv's cutoff; [2 RP^2, 3 RP^2) eigenvector scratch of the RP > 64
+// fallback; the request word at ginv_req (a double: R = replace the inverse
+// by pinv of the saved R x R Gram, 0 = none).
+__host__ __device__ inline int64_t ginv_req(int RP) { return 3 * (int64_t)RP * RP; }
+inline size_t ginv_count(int RP) { return (size_t)ginv_req(RP) + 8; }
+// Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere),
+// plus the pinv request of pinv.h.  flags is unused by the solves since the
+// pinv fallback raises TRITD_FLAG_PINV_TOL itself (kept for the call shape).
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
                   int* flags, const int* stop, hipStream_t st);
-// Y = M * Ginv ([rows][RP]); optional transposed copy YT[k*ldT + i]
+// Y = M * Ginv ([rows][RP]); optional transposed copy YT[k*ldT + i].  A set
+// request word makes every workgroup use pinv(saved Gram) instead (pinv.h);
+// flags[0] is raised when that pinv drops a singular value.
 void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, double* Y, double* YT,
-                  int64_t ldT, const int* stop, hipStream_t st);
+                  int64_t ldT, const int* stop, int* flags, hipStream_t st);
 // ---- Qi model (opts.model='qi', k_qi.hip; origin_triple_tensor/build{F,G,H}.m) ----
 // H[(j*n1p+i)*RP + p+r*q] = sum_s Ah(i, q+r*s) Bh(j, p+r*s)  (zero for k >= R)
 void launch_qi_h(const Geom& g, int r, const double* Ah, const double* Bh, double* H,
@@ -238,8 +249,12 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
 // Y = M * Ginv for any RP; M double or single (Mf); round32: results rounded to
 // single (then stored as double; MATLAB's (X*F')*pinv(G) is single for single
 // data); YT transposed copy, YF single copy (either may be null)
-void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, const double* Ginv,
+// (the pinv fallback runs first, in k_pinv_fix: a one-workgroup launch that
+// returns at once unless the request word is set)
+void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, double* Ginv,
                       double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
-                      hipStream_t st);
+                      int* flags, hipStream_t st);
+// the pinv fallback alone (pinv.h): Ginv[0, RP^2) <- pinv(saved Gram) if requested
+void launch_pinv_fix(int RP, double* Ginv, const int* stop, int* flags, hipStream_t st);
 
 }  // namespace tritd

@@ -182,7 +182,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     // one inverse per Gram slot, kept across iterations: each solve refines
     // the previous inverse of its own slot (k_solve_ns); zero = no start
     for (DBuf* b : {&GinvA_, &GinvB_, &GinvC_}) {
-        b->alloc((size_t)g_.RP * g_.RP);
+        b->alloc(ginv_count(g_.RP));  // inverse + pinv fallback space (pinv.h)
         TRITD_HIP(hipMemsetAsync(b->p, 0, b->bytes(), st_));
     }
     BtB_.alloc((size_t)g_.RP * g_.RP);
@@ -194,7 +194,9 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         launch_fill(ones_.p, (int64_t)ones_.n, 1.0, st_);
         for (DBuf* b : {&GqA_, &GqB_, &GqC_}) b->alloc((size_t)g_.RP * g_.RP);
     }
-    red1_.alloc(red1_count() + 2 * (size_t)k5n());  // + the tail for K5's norm partials
+    k5tail_ = k5n();
+    if (comm_ && comm_->comm) agree_counts();
+    red1_.alloc(red1_count() + 2 * (size_t)k5tail_);  // + the tail for K5's norm partials
     red2_.alloc(red2_count());
     red3_.alloc(2);
     k5part_.alloc(2 * (size_t)k5n());
@@ -397,37 +399,37 @@ void Session::solve(int mode, const double* P, const double* Q, double alpha, do
 
 // (X*F')*pinv(G): fp64 path through the MFMA apply (RP <= 64); fp32
 // path single in, single-rounded out (MATLAB single * double = single)
-void Session::do_apply_A(const double* Ginv) {
+void Session::do_apply_A(double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, nullptr, M1_.f(), g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
-                         true, ctrl_, st_);
+                         true, ctrl_, ctrl_ + 2, st_);
     else if (g_.RP > 64)  // fp64 r = 9..16
         launch_apply_gen(g_.RP, M1_.p, nullptr, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
-                         false, ctrl_, st_);
+                         false, ctrl_, ctrl_ + 2, st_);
     else
-        launch_apply(g_.RP, M1_.p, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, ctrl_, st_);
+        launch_apply(g_.RP, M1_.p, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, ctrl_, ctrl_ + 2, st_);
 }
 
-void Session::do_apply_B(const double* M2, const double* Ginv) {
+void Session::do_apply_B(const double* M2, double* Ginv) {
     if (f32_)
-        launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, true, ctrl_,
+        launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, true, ctrl_, ctrl_ + 2,
                          st_);
     else if (g_.RP > 64)  // fp64 r = 9..16
-        launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, false, ctrl_,
+        launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, false, ctrl_, ctrl_ + 2,
                          st_);
     else
-        launch_apply(g_.RP, M2, g_.n2, Ginv, Bh_.p, nullptr, 0, ctrl_, st_);
+        launch_apply(g_.RP, M2, g_.n2, Ginv, Bh_.p, nullptr, 0, ctrl_, ctrl_ + 2, st_);
 }
 
-void Session::do_apply_C(const double* Ginv) {
+void Session::do_apply_C(double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ChF_.f(),
-                         true, ctrl_, st_);
+                         true, ctrl_, ctrl_ + 2, st_);
     else if (g_.RP > 64)  // fp64 r = 9..16
         launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, nullptr,
-                         false, ctrl_, st_);
+                         false, ctrl_, ctrl_ + 2, st_);
     else
-        launch_apply(g_.RP, red2_.p, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ctrl_, st_);
+        launch_apply(g_.RP, red2_.p, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ctrl_, ctrl_ + 2, st_);
 }
 
 void Session::launch_k5_any(int k, bool prologue) {
@@ -476,6 +478,38 @@ void Session::allreduce(double* buf, int64_t count) {
     if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
 }
 
+// Every rank must issue each all-reduce with the same count.  red1 and red2
+// are fixed by (n2, n3, r); the norm-partial tail of red1 follows the shard
+// height (K5's grid), so it is sized to the largest shard's and the pairs past
+// this rank's own stay zero (k_reduce_finish clears what it consumed).  The
+// schedule itself (maxIter, disp: the print flushes the pending norms) must
+// agree too.  One max-all-reduce of (x, -x) pairs at creation: every rank
+// sees the same result, so a mismatch fails on all of them alike instead of
+// hanging the first collective that differs.
+void Session::agree_counts() {
+    const double c[5] = {(double)k5n(), (double)red1_count(), (double)red2_count(),
+                         (double)o_.maxIter, (double)(o_.disp != 0)};
+    double h[10];
+    for (int q = 0; q < 5; ++q) {
+        h[2 * q] = c[q];
+        h[2 * q + 1] = -c[q];
+    }
+    DBuf v;
+    v.alloc(10);
+    TRITD_HIP(hipMemcpyAsync(v.p, h, sizeof h, hipMemcpyHostToDevice, st_));
+    const ncclResult_t r = ncclAllReduce(v.p, v.p, 10, ncclFloat64, ncclMax, comm_->comm, st_);
+    if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    TRITD_HIP(hipMemcpyAsync(h, v.p, sizeof h, hipMemcpyDeviceToHost, st_));
+    TRITD_HIP(hipStreamSynchronize(st_));
+    k5tail_ = (int)h[0];
+    static const char* what[5] = {"", "n2 or r", "n3 or r", "opts.maxIter", "opts.disp"};
+    for (int q = 1; q < 5; ++q)
+        if (h[2 * q] != -h[2 * q + 1])
+            throw Error(TRITD_ERR_ARG, std::string("ranks disagree on ") + what[q] +
+                                           " (every rank must create its session with the same "
+                                           "n1, n2, n3, r and opts)");
+}
+
 int Session::next_iter() {
     if (k_enq_ >= o_.maxIter) return 0;
     ++k_enq_;
@@ -493,9 +527,9 @@ void Session::set_ah(int k) {
 void Session::flush_norms() {
     if (!norms_pending_) return;
     double* parts = red1_.p + red1_count();
-    allreduce(parts, 2 * (int64_t)k5n());
-    launch_reduce_finish(parts, k5n(), normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
-                         ctrl_, f32_, st_);
+    allreduce(parts, 2 * (int64_t)k5tail_);
+    launch_reduce_finish(parts, k5tail_, normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
+                         ctrl_, f32_, st_, /*clear=*/true);
     norms_pending_ = false;
 }
 
@@ -724,10 +758,10 @@ void Session::iterate_fused(int k) {
         // all-reduce carries K5(k-1)'s norm partials; the finish of k-1
         // follows it, and every kernel after that checks its stop flag.
         const bool pend = norms_pending_;
-        allreduce(red1_.p, red1_count() + (pend ? 2 * (int64_t)k5n() : 0));
+        allreduce(red1_.p, red1_count() + (pend ? 2 * (int64_t)k5tail_ : 0));
         if (pend) {
-            launch_reduce_finish(red1_.p + red1_count(), k5n(), normD_, pend_k_, o_.tol,
-                                 errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_);
+            launch_reduce_finish(red1_.p + red1_count(), k5tail_, normD_, pend_k_, o_.tol,
+                                 errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_, /*clear=*/true);
             norms_pending_ = false;
         }
         solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
@@ -923,9 +957,9 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
     int done = 0, stopped = 0;
     sync(&done, &stopped);
     if (A) {  // the A of the last finished iteration (its parity buffer)
-        const DBuf& a = AhB_[done & 1];
-        std::vector<double> h(a.n);
-        TRITD_HIP(hipMemcpy(h.data(), a.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        std::vector<double> h(AhB_[done & 1].n);
+        TRITD_HIP(hipMemcpy(h.data(), finished_ah(done), h.size() * sizeof(double),
+                            hipMemcpyDeviceToHost));
         unpack_A(g_, h, A);
     }
     if (B) {
@@ -996,7 +1030,7 @@ void Session::rre_parts(const void* dX, int64_t ldX, double* num, double* den) {
     out.alloc(2);
     int done = 0;
     sync(&done, nullptr);
-    const double* ah = AhB_[done & 1].p;  // the A of the last finished iteration
+    const double* ah = finished_ah(done);
     // X(i,j,t) of the shard at src[i + ldX*(j + n2*t)]
     if (qi_) {
         launch_qi_h(g_, g_.r, ah, Bh_.p, H_.p, nullptr, st_);

@@ -108,6 +108,11 @@ class Session {
     bool fused_ = false;
     // K5's norm-partial count (its workgroups; the fp32 rank-split K5 has more)
     int k5n() const { return f32_ ? k5_parts32(g_) : k5_grid(g_); }
+    // pairs in red1_'s norm-partial tail: the largest k5n() over the ranks
+    // (shards of different heights launch different K5 grids, and every rank
+    // must all-reduce the same count); set by agree_counts()
+    int k5tail_ = 0;
+    void agree_counts();
     int k2side_ = 1;  // update_C's solve beside K2 (0: after it, experiments)
     SideSolve k5side_;  // the side solve of the next K5 launch
     // communicator: K5's norm partials of iteration pend_k_ wait in red1_'s
@@ -140,9 +145,9 @@ class Session {
     void do_m2(double* M2);
     void do_m3();
     void do_m3_qi();
-    void do_apply_A(const double* Ginv);
-    void do_apply_B(const double* M2, const double* Ginv);
-    void do_apply_C(const double* Ginv);
+    void do_apply_A(double* Ginv);
+    void do_apply_B(const double* M2, double* Ginv);
+    void do_apply_C(double* Ginv);
     void launch_k5_any(int k, bool prologue);
     bool f32_ = false;
     size_t es_ = sizeof(double);  // bytes per element of D, O, E, Y_L, Y_O, T, W, M1
@@ -173,8 +178,14 @@ class Session {
     // iteration that has already started (the speculative start of
     // iterate_fused with a communicator); Ah_/AhT_ are views of the current one
     DBuf AhB_[2], AhTB_[2];
+    // Ah_/AhT_ are valid only while iterations are being enqueued: after a
+    // run they point at the parity of the last ENQUEUED iteration, which after
+    // a stop (or a speculative iteration of the comm schedule) holds a newer
+    // or partial A.  Readers after run() use finished_ah().
     DBuf Ah_, AhT_, Bh_, Ch_, ChT_, M1_, BtB_, CtC_;
     void set_ah(int k);
+    // A^ of the last finished iteration `done` (as returned by sync)
+    const double* finished_ah(int done) const { return AhB_[done & 1].p; }
     // Qi model (opts.model = TRITD_MODEL_QI, k_qi.hip): H = the Qi mode-3 design
     // matrix by rows ij (K2/K5 Khatri-Rao operand), an all-ones RP x RP block
     // (the Hadamard factor of the solve and the B operand of the KR product),

@@ -7,6 +7,7 @@
 #include <utility>
 
 #include "kernels.h"
+#include "pinv.h"
 
 namespace tritd {
 
@@ -57,8 +58,9 @@ __device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, doubl
 // kernel's block): RP/NW rows per lane, lane = column (k_solve's algorithm
 // and rounding with another row split).  rowbuf: 2*NW*64 doubles, pivs: RP
 // doubles of LDS.
-// Ginv is written directly (R x R block, zero pad); the pinv-tolerance check
-// of k_solve raises flags[0].
+// Ginv is written directly (R x R block, zero pad), with the pinv request of
+// pinv.h (the consumer replaces the inverse by pinv when the pivots come near
+// MATLAB's cutoff).
 template <int RP, int NW = 4>
 __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, double* pivs) {
     // the host kernel's other workgroups share this CU's SIMDs: win issue
@@ -84,15 +86,8 @@ __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, d
             const int i = RW * w + q;
             s.Ginv[i * RP + c] = (i < s.R && c < s.R) ? -a[q] : 0.0;
         }
-    if (threadIdx.x == 0) {
-        double minpiv = 1e308, maxpiv = 0.0;
-        for (int p = 0; p < s.R; ++p) {
-            minpiv = fmin(minpiv, pivs[p]);
-            maxpiv = fmax(maxpiv, pivs[p]);
-        }
-        const double tol = (double)s.R * ldexp(1.0, ilogb(maxpiv) - 52);  // pinv: R*eps(max)
-        if (!(minpiv > 1e3 * tol)) atomicOr(s.flags, 1);
-    }
+    // pinv's cutoff near: save the Gram and request the fallback (pinv.h)
+    pinv_request<64 * NW>(pivots_near_cutoff(pivs, s.R), s.P, s.Q, s.R, RP, s.alpha, s.Ginv);
 }
 
 }  // namespace tritd
