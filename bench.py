@@ -28,13 +28,18 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA, dense
+F64_MFMA_PEAK_TFS = 78.6  # MI355X_MICROARCH.md: f64 MFMA, dense
 # SURVEY.md §8d workloads: (n1, n2, n3, r, dtype)
 CONFIGS = {4: (512, 512, 512, 8, "f64"), 5: (2048, 2048, 256, 16, "f32")}
 
 
 def ensure_built():
-    if not os.path.exists(os.path.join(PKG, "tritd", "libtritd.so")):
-        subprocess.run(["make", "-j8", "-C", os.path.join(PKG, "csrc")], check=True)
+    """Rebuild libtritd.so when any source or header is newer than it (make's
+    own dependency check), so a stale library is never benchmarked as HEAD."""
+    csrc = os.path.join(PKG, "csrc")
+    if subprocess.run(["make", "-q", "-C", csrc], stdout=subprocess.DEVNULL,
+                      stderr=subprocess.DEVNULL).returncode != 0:
+        subprocess.run(["make", "-j8", "-C", csrc], check=True, stdout=subprocess.DEVNULL)
 
 
 def cpu_baseline(D, r, opts, A0, B0, C0, iters):
@@ -64,6 +69,60 @@ def cpu_baseline(D, r, opts, A0, B0, C0, iters):
                 "sample": "unavailable: %s" % e}
 
 
+def end_to_end(tritd, D, r, opts, A0, B0, C0, device):
+    """Wall time of one triple_decomp_ADMM(D, r, opts) call with maxIter = 100
+    from host arrays to host arrays — what the reference's drivers time with
+    tic/toc around the solver (traffic_triple_comparison.m:51,61; README.md:63):
+    session creation (placement probe, D upload, tile-major conversion), the
+    loop, and get (factors, O, E and errHist back to the host).  The one-shot
+    call does not probe placements (TRITD_SESSION_PROBE is a session option);
+    the same call with the probe forced (TRITD_PROBE=8) is timed beside it,
+    interleaved, two calls each (min reported), so the probe's net effect on a
+    one-shot solve stays visible."""
+    o = dict(opts, maxIter=100)
+    old = os.environ.get("TRITD_PROBE")
+    times = {"default": [], "with_probe": []}
+    k = None
+    try:
+        for rep in range(2):
+            for label, val in (("default", old), ("with_probe", "8")):
+                if val is None:
+                    os.environ.pop("TRITD_PROBE", None)
+                else:
+                    os.environ["TRITD_PROBE"] = val
+                t0 = time.perf_counter()
+                out = tritd.triple_decomp_ADMM(D, r, o, A0, B0, C0, device=device,
+                                               return_iters=True)
+                times[label].append((time.perf_counter() - t0) * 1e3)
+                k = out[-1]
+                del out
+    finally:
+        if old is None:
+            os.environ.pop("TRITD_PROBE", None)
+        else:
+            os.environ["TRITD_PROBE"] = old
+    res = {"maxIter": 100, "k": k, "unit": "ms"}
+    for label, t in times.items():
+        res[label] = {"ms": min(t), "ms_each": [round(x, 2) for x in t]}
+    res["ms"] = res["default"]["ms"]
+    res["probe_net_ms"] = res["with_probe"]["ms"] - res["default"]["ms"]
+    return res
+
+
+def pmc_mfma_util(config):
+    """K2's MFMA utilisation from the committed rocprofv3 SQ pass
+    (tools/pmc_summary.py --json -> profiles/*_k2_mfma_util.json):
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)."""
+    import glob
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*k2_mfma_util.json"))
+                   if ("_c5_" in os.path.basename(f)) == (config == 5))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("mfma_util"), os.path.relpath(files[-1], ROOT)
+
+
 def pmc_traffic(config):
     """HBM bytes per fused-update launch from the committed rocprofv3 PMC pass
     (tools/pmc_traffic.py -> profiles/*_k5_traffic.json, config 5:
@@ -89,6 +148,7 @@ def main():
     # bounded host sample: ~20 s at config 4, one iteration at config 5 (§8d)
     ap.add_argument("--cpu-iters", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end one-shot calls")
     # --algo als: triple_decomp_ALS.m on the config-4 workload
     ap.add_argument("--algo", default="admm", choices=("admm", "als"))
     args = ap.parse_args()
@@ -231,6 +291,24 @@ def main():
                  "e_dense_tiles_per_launch": dense_per_launch,
                  "e_tiles_per_launch": tiles_per_launch})
 
+    # K2 (the mode-3 MTTKRP, X3*H' of :93): the RPAS GEMM north_star prices
+    # against the MFMA peak; 2 * N_local * R flops per launch
+    k2_ms = km["mode3"]
+    k2_flops = 2.0 * N_local * r * r
+    k2_tfs = k2_flops / (k2_ms * 1e-3) / 1e12 if k2_ms > 0 else None
+    k2_peak = F32_MFMA_PEAK_TFS if f32 else F64_MFMA_PEAK_TFS
+    pmc_util, pmc_src = pmc_mfma_util(args.config) if world == 1 else (None, None)
+    roof["mfma_gemm"] = {"kernel": "k_m3_cp (mode-3 MTTKRP, X3*H' of triple_decomp_ADMM.m:93)",
+                         "achieved": k2_tfs, "peak": k2_peak, "unit": "TFLOP/s",
+                         "frac": (k2_tfs / k2_peak) if k2_tfs else None,
+                         "algorithmic_flops_per_launch": k2_flops, "ms": k2_ms,
+                         "pmc_mfma_util": pmc_util, "pmc_source": pmc_src}
+
+    sess.close()
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = end_to_end(tritd, D, r, opts, data["A0"], data["B0"], data["C0"], local_rank)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], cpu_iters)
@@ -264,10 +342,12 @@ def main():
             # candidate tensor pools timed with K5's access pattern at session
             # creation (rank 0), the fastest kept
             "placement_probe": {"ms": [round(m, 4) for m in probe_ms], "picked": probe_pick},
+            # one whole triple_decomp_ADMM call (maxIter=100), host arrays in and out,
+            # timed like the drivers' tic/toc (traffic_triple_comparison.m:51,61)
+            "end_to_end": e2e,
         }
         print(json.dumps(line), flush=True)
 
-    sess.close()
     if comm is not None:
         comm.close()
     if dist is not None:

@@ -80,10 +80,11 @@ typedef void (*tritd_print_fn)(const char* line, void* user);
 
 /* Warning flags (bitmask).  Not errors: the call succeeded and its outputs
  * are valid, but they may differ from the reference's beyond rounding.
- * TRITD_FLAG_PINV_TOL: an R x R ridge Gram's smallest pivot came within 1e3x
- * of MATLAB's pinv tolerance max(size)*eps(max sigma)
- * (triple_decomp_ADMM.m:78,86,93; triple_decomp_ALS.m:27,32,37): pinv could
- * have truncated singular values there, the GPU's inverse does not. */
+ * TRITD_FLAG_PINV_TOL: MATLAB's pinv (triple_decomp_ADMM.m:78,86,93;
+ * triple_decomp_ALS.m:27,32,37) truncated an R x R ridge Gram here: a solve's
+ * smallest pivot came within 1e3x of pinv's tolerance max(size)*eps(max sigma),
+ * the device formed pinv of that Gram (Jacobi eigensolver with MATLAB's
+ * tolerance) and it dropped at least one singular value. */
 enum { TRITD_FLAG_PINV_TOL = 1u };
 
 const char* tritd_version(void);
@@ -132,7 +133,11 @@ typedef struct tritd_comm tritd_comm;
 
 enum {
     TRITD_SESSION_D_ON_DEVICE = 1, /* D is a device pointer on `device` */
-    TRITD_SESSION_F32 = 2          /* D is float (class single): the fp32 data path */
+    TRITD_SESSION_F32 = 2,         /* D is float (class single): the fp32 data path */
+    TRITD_SESSION_PROBE = 4        /* choose where the tensor pool lives by timing the fused
+                                      update's access pattern on up to 16 candidate allocations
+                                      (~5-10 % on that kernel; pays off over hundreds of
+                                      iterations, so the one-shot calls never do it) */
 };
 
 /* D points at D(i0,0,0) (double, or float with TRITD_SESSION_F32); consecutive (j,t) fibres are ldD elements apart

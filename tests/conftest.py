@@ -37,11 +37,33 @@ def load_golden(name):
     return d
 
 
+def _flat(x):
+    """Memory-order view (no copy for C- or F-contiguous arrays; a plain
+    ravel() of a column-major array copies it in C order)."""
+    return np.asarray(x).ravel(order="K") if np.asarray(x).flags.forc else np.asarray(x).ravel()
+
+
+def sumsq_diff(a, b, chunk=1 << 24):
+    """(sum (a-b)^2, sum b^2) in float64, chunked: full-size tensors (1e9
+    elements) without float64 temporaries of their whole size."""
+    a, b = _flat(a), _flat(b)
+    assert a.shape == b.shape
+    num = den = 0.0
+    for s in range(0, a.size, chunk):
+        x = a[s:s + chunk].astype(np.float64)
+        y = b[s:s + chunk].astype(np.float64)
+        num += float(np.dot(x - y, x - y))
+        den += float(np.dot(y, y))
+    return num, den
+
+
 def rel(a, b):
-    a = np.asarray(a, dtype=np.float64)
-    b = np.asarray(b, dtype=np.float64)
-    nb = np.linalg.norm(b.ravel())
-    return np.linalg.norm((a - b).ravel()) / (nb if nb > 0 else 1.0)
+    a, b = np.asarray(a), np.asarray(b)
+    if a.flags.forc != b.flags.forc or (a.flags.f_contiguous != b.flags.f_contiguous):
+        a = np.asarray(a, order="F")
+        b = np.asarray(b, order="F")
+    num, den = sumsq_diff(a, b)
+    return float(np.sqrt(num) / (np.sqrt(den) if den > 0 else 1.0))
 
 
 @pytest.fixture(scope="session")

@@ -9,7 +9,7 @@ TAG=${1:-r01}
 ALG=${2:-32212254720}   # K5 algorithmic bytes per launch at config 5 without dense E tiles
 O=gpurun_out/${TAG}_c5
 mkdir -p $O
-B="python3 bench.py --config 5 --no-cpu --steps 3 --warmup 1"
+B="python3 bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- \
     $B > $O/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- \
@@ -17,6 +17,6 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write
 python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/${TAG}_c5_k5_traffic.json $ALG "k5_f32s<256>" 1:4  # timed window (warmup 1, steps 3): E densifies later
 cp $O/${TAG}_c5_k5_traffic.json profiles/${TAG}_c5_k5_traffic.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
-    python3 bench.py --config 5 --no-cpu --steps 10 --warmup 3 > $O/stats.log 2>&1
+    python3 bench.py --config 5 --no-cpu --no-e2e --steps 10 --warmup 3 > $O/stats.log 2>&1
 timeout -k 10 500 python3 bench.py --config 5 --steps 10 --warmup 3 > $O/${TAG}_c5_bench_line.json 2> $O/bench.err
 cat $O/${TAG}_c5_bench_line.json

@@ -296,7 +296,7 @@ void AlsSession::sync(int* done, int* stopped) {
     if (!ev_.empty()) harvest_timing();
     int ctrl[3];
     TRITD_HIP(hipMemcpy(ctrl, ctrl_, 3 * sizeof(int), hipMemcpyDeviceToHost));
-    if (ctrl[2]) flags_ |= TRITD_FLAG_PINV_TOL;  // a solve's pivot neared pinv's cutoff
+    if (ctrl[2] & 1) flags_ |= TRITD_FLAG_PINV_TOL;  // the pinv fallback dropped a value
     if (done) *done = ctrl[1];
     if (stopped) *stopped = ctrl[0];
 }

@@ -1097,6 +1097,182 @@ static size_t solve_big_lds(int RP) {
 }
 
 // ---------------------------------------------------------------------------
+// Ginv = inv(P o Q + alpha I) at RP = 128 / 256 across NB = RP/16 workgroups
+// (k_solve_mw): the blocked symmetric sweep of k_solve_big, with S split
+// into row strips.  k_solve_big keeps S in one workgroup and moves all of it
+// through that CU's LDS/L2 port on every block step (0.75 ms at RP = 256,
+// on the critical path of config 5's update_B, triple_decomp_ADMM.m:86).
+// Here workgroup b owns rows [16b, 16b+16) in its LDS (32 KB at 256) and
+// block step K is:
+//   owner (b = K): M = inv(S_KK) (one wave, register sweep: the sequential
+//     sweep's pivots, kept for the pinv-tolerance test), X = M S_K,: (f64
+//     MFMA), S_K,: <- X except S_KK <- -M; publishes X and its 16 pivots
+//     (global scratch of its Ginv buffer) and then step word K = epoch;
+//   others: wait for step word K, then S_I,j -= S_IK X_Kj (f64 MFMA, the old
+//     S_IK from registers) and S_IK <- (X_K,I)^T.
+// The arithmetic is k_solve_big's (same blocks, same order per block), so
+// the accuracy is too.  Cross-workgroup order: the owner's stores, an agent-
+// scope release fence, a barrier and a release store of the step word; the
+// waiter's acquire load of it, a barrier and an agent-scope acquire fence in
+// every thread.  Only workgroup 0 reads the stop flag; a stopped launch
+// publishes step word 0 with the stop bit, so all workgroups agree (a flag
+// set mid-launch by another stream could not split them).  The workgroups
+// depend only on earlier steps (acyclic), so a workgroup dispatched late —
+// the GPU busy with K5 on another stream — delays the chain but cannot
+// deadlock it; a wait longer than ~1 s still gives up (flags bit 2, which
+// the session turns into an error) rather than hang the GPU.
+// Epochs (host counter, < 2^31, never 0) make the step words single-use
+// without a reset.
+// ---------------------------------------------------------------------------
+constexpr int MW_NT = 256;  // 4 waves per workgroup
+constexpr unsigned MW_STOP = 0x80000000u;
+
+__device__ __forceinline__ unsigned mw_wait(const unsigned* w, unsigned epoch, int* flags) {
+    unsigned v = 0;
+    for (int n = 0;; ++n) {
+        v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & ~MW_STOP) == epoch) return v;
+        if (n > (1 << 22)) {  // ~1 s of polls: give up, never hang the device
+            atomicOr(flags, 2);
+            return MW_STOP;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <int RP>
+__global__ __launch_bounds__(MW_NT) void k_solve_mw(const double* __restrict__ P,
+                                                  const double* __restrict__ Q, int R,
+                                                  double alpha, double* Ginv, int* flags,
+                                                  const int* stop, unsigned epoch) {
+    constexpr int NB = RP / SB, LD = RP + 2, TPW = NB / (MW_NT / 64);  // column tiles per wave
+    static_assert(NB % (MW_NT / 64) == 0, "column tiles split evenly over the waves");
+    __shared__ double St[SB * LD];  // this workgroup's strip of S
+    __shared__ double Ml[SB * (SB + 1)];
+    __shared__ double rowp[64];
+    __shared__ double pvl[SB];
+    __shared__ unsigned state;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m = lane & 15, kq = lane >> 4;
+    const int b = blockIdx.x, i0 = SB * b;
+    double* Xg = Ginv + 2 * (int64_t)RP * RP;  // [NB][SB][RP]: X of every step (pinv.h scratch, free here)
+    double* pivg = Ginv + ginv_piv(RP);
+    unsigned* sync = reinterpret_cast<unsigned*>(Ginv + ginv_sync(RP));
+    // the launch's stop decision, workgroup 0's alone
+    if (b == 0 && tid == 0) state = (*stop) ? MW_STOP : 0u;
+    if (b == 0) {
+        __syncthreads();
+        if (state) {
+            if (tid == 0) __hip_atomic_store(&sync[0], epoch | MW_STOP, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    // strip rows i0..i0+15 of S = P o Q + alpha I (R x R block), identity pad
+    for (int e = tid; e < SB * RP; e += MW_NT) {
+        const int r = e / RP, c = e - (e / RP) * RP, i = i0 + r;
+        double v;
+        if (i < R && c < R) {
+            v = P[(int64_t)i * RP + c] * Q[(int64_t)i * RP + c];
+            if (i == c) v = v + alpha;
+        } else {
+            v = (i == c) ? 1.0 : 0.0;
+        }
+        St[r * LD + c] = v;
+    }
+    __syncthreads();
+    for (int K = 0; K < NB; ++K) {
+        const int k0 = SB * K;
+        double* XK = Xg + (int64_t)K * SB * RP;
+        if (b == K) {
+            // M = inv(S_KK): wave 0 sweeps the block in registers (k_solve_big's sweep)
+            if (w == 0) {
+                const int cc = lane & (SB - 1);
+                double a[SB];
+#pragma unroll
+                for (int i = 0; i < SB; ++i) a[i] = St[i * LD + k0 + cc];
+                sweep32_all(a, rowp, pvl, cc, std::make_integer_sequence<int, SB>{});
+#pragma unroll
+                for (int i = 0; i < SB; ++i) Ml[i * (SB + 1) + cc] = -a[i];
+            }
+            __syncthreads();
+            // X = M S_K,: : tile jt, A[m][k] = M(m, 4s+k), B[k][n] = S(k0+4s+k, 16jt+n)
+            d4 x[TPW];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                const int jt = w + (MW_NT / 64) * u;
+                d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s4 = 0; s4 < SB / 4; ++s4)
+                    acc = mfma4(Ml[m * (SB + 1) + 4 * s4 + kq], St[(4 * s4 + kq) * LD + 16 * jt + m], acc);
+                x[u] = acc;
+            }
+            __syncthreads();  // every B operand read before the strip is overwritten
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                const int jt = w + (MW_NT / 64) * u;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = kq + 4 * r, col = 16 * jt + m;
+                    XK[row * RP + col] = x[u][r];
+                    St[row * LD + col] = (jt == K) ? -Ml[row * (SB + 1) + m] : x[u][r];
+                }
+            }
+            if (tid < SB) pivg[k0 + tid] = pvl[tid];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&sync[K], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (tid == 0) state = mw_wait(&sync[K], epoch, flags);
+            // old S_IK as the A operands (A[m][k] = -S(i0+m, k0+4s+k)) before any write
+            double a[SB / 4];
+#pragma unroll
+            for (int s4 = 0; s4 < SB / 4; ++s4) a[s4] = -St[m * LD + k0 + 4 * s4 + kq];
+            __syncthreads();
+            if (state & MW_STOP) return;  // stopped launch (or a timed-out wait)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                const int jt = w + (MW_NT / 64) * u;
+                if (jt == K) {
+                    // S_IK <- (X_K,I)^T: element (row kq+4r, col k0+m) = X(m, i0+kq+4r)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) St[(kq + 4 * r) * LD + k0 + m] = XK[m * RP + i0 + kq + 4 * r];
+                } else {
+                    d4 acc;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[r] = St[(kq + 4 * r) * LD + 16 * jt + m];
+#pragma unroll
+                    for (int s4 = 0; s4 < SB / 4; ++s4)
+                        acc = mfma4(a[s4], XK[(4 * s4 + kq) * RP + 16 * jt + m], acc);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) St[(kq + 4 * r) * LD + 16 * jt + m] = acc[r];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // S = -inv: Ginv rows i0.. = -S, pad zeroed
+    for (int e = tid; e < SB * RP; e += MW_NT) {
+        const int r = e / RP, c = e - (e / RP) * RP, i = i0 + r;
+        Ginv[(int64_t)i * RP + c] = (i < R && c < R) ? -St[r * LD + c] : 0.0;
+    }
+    // the last owner has acquired every earlier step, so it sees every pivot
+    if (b == NB - 1) {
+        __shared__ double pall[RP];
+        for (int p = tid; p < RP; p += MW_NT) pall[p] = pivg[p];
+        __syncthreads();
+        pinv_request<MW_NT>(pivots_near_cutoff(pall, R), P, Q, R, RP, alpha, Ginv);
+    }
+}
+
+static unsigned mw_epoch() {
+    static unsigned e = 0;
+    e = (e + 1) & ~MW_STOP;
+    if (e == 0) e = 1;
+    return e;
+}
+
+// ---------------------------------------------------------------------------
 // Ginv = inv(P o Q + alpha I) at RP = 128 (fp32 path, r = 9..11): blocked
 // symmetric sweep with the matrix S in LDS (153 KB).  Per block K of 16
 // pivots (k0 = 16K):
@@ -1255,16 +1431,17 @@ void launch_solve_blk(int R, const double* P, const double* Q, double alpha, dou
 }
 
 // RP <= 64: Newton-Schulz refinement of the previous inverse with the
-// per-pivot sweep as fallback (k_solve_ns); RP = 128: blocked sweep
-// (k_solve_blk); RP = 256: k_solve_big.  TRITD_SOLVE=gj runs the plain sweep
+// per-pivot sweep as fallback (k_solve_ns); RP = 128 / 256: the multi-
+// workgroup blocked sweep (k_solve_mw).  TRITD_SOLVE=gj runs the plain sweep
 // (k_solve) at RP <= 64, =blk the blocked sweep there (timing / accuracy
-// experiments), =sweep keeps k_solve_big at 128.
+// experiments), =big the one-workgroup kernels at 128 / 256 (k_solve_blk /
+// k_solve_big), =sweep k_solve_big at both.
 static int solve_mode() {
     static const int v = [] {
         const char* e = std::getenv("TRITD_SOLVE");
         if (!e) return 0;
         const std::string x(e);
-        return x == "blk" ? 1 : (x == "sweep" ? 2 : (x == "gj" ? 3 : 0));
+        return x == "blk" ? 1 : (x == "sweep" ? 2 : (x == "gj" ? 3 : (x == "big" ? 4 : 0)));
     }();
     return v;
 }
@@ -1276,6 +1453,17 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
         hipLaunchKernelGGL(k_solve<RPV>, dim3(1), dim3(RPV * 64 / SOLVE_ROWS), 0, st, P, Q, R, alpha, \
                            Ginv, flags, stop);                                               \
         break;
+    if ((RP == 128 || RP == 256) && (solve_mode() == 0 || solve_mode() == 3)) {
+        // multi-workgroup blocked sweep (k_solve_mw): RP/16 workgroups
+        if (RP == 128)
+            hipLaunchKernelGGL(k_solve_mw<128>, dim3(128 / SB), dim3(MW_NT), 0, st, P, Q, R, alpha,
+                               Ginv, flags, stop, mw_epoch());
+        else
+            hipLaunchKernelGGL(k_solve_mw<256>, dim3(256 / SB), dim3(MW_NT), 0, st, P, Q, R, alpha,
+                               Ginv, flags, stop, mw_epoch());
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     if ((RP == 128 && solve_mode() != 2) || (RP <= 64 && solve_mode() == 1)) {
         switch (RP) {
             case 16: launch_solve_blk<16>(R, P, Q, alpha, Ginv, flags, stop, st); break;

@@ -98,8 +98,12 @@ void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* st
 // near pinv's cutoff; [2 RP^2, 3 RP^2) eigenvector scratch of the RP > 64
 // fallback; the request word at ginv_req (a double: R = replace the inverse
 // by pinv of the saved R x R Gram, 0 = none).
+// Past the request word: RP pivots and RP/16 step words of the multi-workgroup
+// solve (k_solve_mw, RP = 128 / 256; zero-initialised with the buffer).
 __host__ __device__ inline int64_t ginv_req(int RP) { return 3 * (int64_t)RP * RP; }
-inline size_t ginv_count(int RP) { return (size_t)ginv_req(RP) + 8; }
+__host__ __device__ inline int64_t ginv_piv(int RP) { return ginv_req(RP) + 8; }
+__host__ __device__ inline int64_t ginv_sync(int RP) { return ginv_piv(RP) + RP; }
+inline size_t ginv_count(int RP) { return (size_t)ginv_sync(RP) + 16; }
 // Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere),
 // plus the pinv request of pinv.h.  flags is unused by the solves since the
 // pinv fallback raises TRITD_FLAG_PINV_TOL itself (kept for the call shape).

@@ -79,6 +79,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     TRITD_HIP(hipSetDevice(device_));
     g_ = make_geom(n1, n2, n3, i0, i1, r);
     f32_ = (flags & TRITD_SESSION_F32) != 0;
+    probe_ = (flags & TRITD_SESSION_PROBE) != 0;
     es_ = f32_ ? sizeof(float) : sizeof(double);
     // fp32 path and fp64 r = 9..16: padded ranks 16/32/48/64/128/256 (the
     // K5 / K2 instantiations; fp64 RP = 128/256 runs K5 at one wave per SIMD
@@ -573,10 +574,14 @@ void Session::phaseC(int k) {
 // allocation in three fast; tools/aos_pattern.hip).  With room to spare,
 // allocate up to TRITD_PROBE (default 8) candidate pools at once, time K5's
 // access pattern on each and keep the fastest.  Results do not depend on the choice (addresses never enter the
-// arithmetic).  Small problems skip it.
+// arithmetic).  Small problems skip it.  Only sessions created with
+// TRITD_SESSION_PROBE probe: the one-shot calls (the MATLAB drop-in) do not,
+// since a 100-iteration solve loses more to the probe than K5 gains
+// (bench.py end_to_end: +17 ms at config 4, +5.7 s at config 5, round 5).
+// TRITD_PROBE=n overrides either way (1 = off).
 double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     const char* pe = std::getenv("TRITD_PROBE");
-    int want = pe ? std::atoi(pe) : 8;
+    int want = pe ? std::atoi(pe) : (probe_ ? 8 : 1);
     // (small pools too: a mode-1 shard of 64 rows at 512^3 is a 0.8 GB pool, and
     // the slowest of P ranks sets the sharded iteration)
     if (pool_bytes < ((size_t)128 << 20)) want = 1;
@@ -927,7 +932,9 @@ void Session::sync(int* done, int* stopped) {
     if (!ev_.empty()) harvest_timing();
     int ctrl[3];
     TRITD_HIP(hipMemcpy(ctrl, ctrl_, 3 * sizeof(int), hipMemcpyDeviceToHost));
-    if (ctrl[2]) flags_ |= TRITD_FLAG_PINV_TOL;  // a solve's pivot neared pinv's cutoff
+    if (ctrl[2] & 1) flags_ |= TRITD_FLAG_PINV_TOL;  // the pinv fallback dropped a value
+    if (ctrl[2] & 2)  // k_solve_mw: a workgroup gave up waiting for a peer (never expected)
+        throw Error(TRITD_ERR_HIP, "multi-workgroup R x R solve: a peer workgroup never arrived");
     if (done) *done = ctrl[1];
     if (stopped) *stopped = ctrl[0];
 }

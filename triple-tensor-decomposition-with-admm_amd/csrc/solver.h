@@ -199,6 +199,7 @@ class Session {
     DBuf k5part_, m3part_, sqpart_;
     DBuf errHist_, errL_, errO_;
     uint32_t flags_ = 0;
+    bool probe_ = false;  // TRITD_SESSION_PROBE: time candidate pools at creation
     int* ctrl_ = nullptr;  // [0] stop, [1] k done, [2] pinv-tolerance flag, then DENSE_SLOTS u64 dense-E counters
     unsigned long long* dense_tiles() const {
         return reinterpret_cast<unsigned long long*>(ctrl_ + 4);

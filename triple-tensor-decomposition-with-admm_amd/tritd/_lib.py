@@ -24,6 +24,7 @@ OPT_BITS = {"mu": OPT_MU, "rho": OPT_RHO, "lambda": OPT_LAMBDA, "lambda2": OPT_L
 MODELS = {"cp": 0, "qi": 1}  # opts.model: TRITD_MODEL_CP / TRITD_MODEL_QI (include/tritd.h)
 SESSION_D_ON_DEVICE = 1
 SESSION_F32 = 2
+SESSION_PROBE = 4
 FLAG_PINV_TOL = 1  # TRITD_FLAG_PINV_TOL (include/tritd.h)
 
 

@@ -389,10 +389,13 @@ class Session:
 
     D is either a host numpy array holding the shard (column-major, leading
     dimension ldD) or, with ``d_device_ptr``, a device pointer.  ``dtype``
-    float32 (or a float32 D) selects the single-class path."""
+    float32 (or a float32 D) selects the single-class path.  ``probe``
+    (default True) times candidate placements of the tensor pool at creation
+    and keeps the fastest (TRITD_SESSION_PROBE): worth it for a session that
+    runs hundreds of iterations, not for one solve."""
 
     def __init__(self, r, opts, A0, B0, C0, *, n1, n2, n3, i0=0, i1=None, D=None,
-                 d_device_ptr=None, ldD=None, device=0, comm=None, dtype=None):
+                 d_device_ptr=None, ldD=None, device=0, comm=None, dtype=None, probe=True):
         self._s = C.c_void_p()
         o = make_opts(opts)
         i1 = n1 if i1 is None else i1
@@ -403,6 +406,8 @@ class Session:
             dtype = np.asarray(D).dtype if D is not None else np.float64
         self.f32 = np.dtype(dtype) == np.float32
         flags = _lib.SESSION_F32 if self.f32 else 0
+        if probe:
+            flags |= _lib.SESSION_PROBE
         if d_device_ptr is not None:
             dptr = C.c_void_p(int(d_device_ptr))
             flags |= _lib.SESSION_D_ON_DEVICE
