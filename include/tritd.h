@@ -207,6 +207,16 @@ void tritd_session_destroy(tritd_session* s);
 tritd_status tritd_comm_unique_id(void* id128);
 tritd_status tritd_comm_create(tritd_comm** out, const void* id128, int32_t nranks, int32_t rank,
                                int32_t device);
+/* Host transport: every all-reduce of a session using this comm drains the
+ * session's stream, copies the buffer to the host and calls fn(buf, count, op,
+ * user) (op 0 = sum, 1 = max; return 0 on success), then copies it back.  For
+ * hosts that own a collective layer already (MPI, gloo) and for running the
+ * multi-rank schedule with several ranks on one GPU (RCCL refuses a GPU twice
+ * in one communicator).  tritd_comm_create (RCCL, device-side, asynchronous)
+ * is the fast path. */
+typedef int32_t (*tritd_allreduce_fn)(double* buf, int64_t count, int32_t op, void* user);
+tritd_status tritd_comm_create_host(tritd_comm** out, tritd_allreduce_fn fn, void* user,
+                                    int32_t nranks, int32_t rank, int32_t device);
 void tritd_comm_destroy(tritd_comm* c);
 
 /* Device set of the one-shot entry points (the MEX host

@@ -65,4 +65,6 @@ def test_video_triple_branch(synth, tmp_path):
     assert res["tnrmse"] == pytest.approx(tn, rel=1e-6)
     assert np.isnan(res["nrmse"])  # no missing entries: 0/0 like MATLAB
     assert os.path.exists(tmp_path / "highway_triple_re_O.mat")
+    from scipy.io import loadmat  # video_triple_comparison.m:32 save(..._raw.mat, 'Y')
+    np.testing.assert_array_equal(loadmat(tmp_path / "highway_raw.mat")["Y"], d["D"])
     assert "PSNR: " in lines[-1] and "SSIM: " in lines[-1]

@@ -1,0 +1,143 @@
+"""The library's own multi-rank schedule with real ranks on one GPU.
+
+RCCL refuses one GPU twice in a communicator, so these tests give libtritd a
+host transport (tritd_comm_create_host: each all-reduce drains the session
+stream and runs torch.distributed over gloo on a host copy).  Everything else
+is the code path `bench.py --gpus N` runs: the sharded iterate_fused
+schedule of solver.cpp (two all-reduces per iteration, K5's norm partials in
+red1's tail sized to the largest shard, the stop test deferred behind the
+next iteration's speculative M1 .. M2), agree_counts at session creation, and
+for ALS the als.cpp schedule.  Shards are uneven and straddle 16 rows (n1 = 33
+on 2 ranks: 17 | 16; n1 = 49 on 3 ranks: 17 | 16 | 16), so the ranks launch
+different K5 grids.  Results must match the oracle's unsharded solve
+(triple_decomp_ADMM.m:15-68) at the tolerances of test_gpu_parity.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ORACLE, PKG, load_golden, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _case(n1, stop, disp=False):
+    from tritd import synth
+    d = synth.low_rank_plus_outliers(n1, 10, 8, 2, seed=5, init_seed=9)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=30, tol=0.2 if stop else 1e-5, disp=int(disp))
+    return d, opts
+
+
+def _worker(rank, world, port, spec, outdir):
+    import sys
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import tritd
+    from tritd.dist import make_host_comm, shard_bounds
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kind = spec["kind"]
+    if "golden" in spec:
+        z = load_golden(spec["golden"])
+        D = z["D"] if kind == "admm" else z["X"]
+        r, opts, A0, B0, C0 = int(z["r"]), z["opts"], z["A0"], z["B0"], z["C0"]
+    else:
+        d, opts = _case(spec["n1"], spec["stop"], spec.get("disp", False))
+        D, r, A0, B0, C0 = d["D"], 2, d["A0"], d["B0"], d["C0"]
+    n1, n2, n3 = D.shape
+    i0, i1 = shard_bounds(n1, world, rank)
+    comm = make_host_comm(dist, rank, world, 0)
+    Dl = np.asfortranarray(D[i0:i1])
+    if kind == "admm":
+        s = tritd.Session(r, opts, A0, B0, C0, n1=n1, n2=n2, n3=n3, i0=i0, i1=i1, D=Dl, device=0,
+                          comm=comm, probe=False)
+    else:
+        s = tritd.AlsSession(r, opts, A0, B0, C0, n1=n1, n2=n2, n3=n3, i0=i0, i1=i1, X=Dl,
+                             device=0, comm=comm)
+    s.run(int(opts["maxIter"]))
+    s.sync()
+    res = s.get()
+    s.close()
+    comm.close()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), i0=i0, i1=i1,
+             **{k: v for k, v in res.items() if k != "k"}, k=res["k"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(tmp_path, world, spec):
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(world, _free_port(), spec, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    return [np.load(tmp_path / f"rank{q}.npz") for q in range(world)]
+
+
+def _assemble(zs, shapeA, shapeO=None):
+    A = np.zeros(shapeA, order="F")
+    O = E = None
+    if shapeO is not None:
+        O = np.zeros(shapeO, order="F")
+        E = np.zeros(shapeO, order="F")
+    for z in zs:
+        i0, i1 = int(z["i0"]), int(z["i1"])
+        A[i0:i1] = z["A"][i0:i1]
+        if O is not None:
+            O[i0:i1], E[i0:i1] = z["O"], z["E"]
+    return A, O, E
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world,n1,stop,disp", [(2, 33, False, False), (2, 33, True, True),
+                                                (3, 49, False, False), (3, 49, True, False)])
+def test_library_schedule_uneven_ranks_match_oracle(tmp_path, world, n1, stop, disp):
+    import tritd_oracle as orc
+    d, opts = _case(n1, stop, disp)
+    rA, rB, rC, rO, reh, rE, rk, _ = orc.triple_decomp_ADMM(d["D"], 2, opts, d["A0"], d["B0"],
+                                                            d["C0"], printer=lambda s: None)
+    assert (rk < 30) == stop
+    zs = _run(tmp_path, world, dict(kind="admm", n1=n1, stop=stop, disp=disp))
+    for z in zs:
+        assert int(z["k"]) == rk
+        np.testing.assert_allclose(z["errHist"], reh, rtol=1e-8, atol=1e-13)
+        assert rel(z["B"], rB) < 1e-8 and rel(z["C"], rC) < 1e-8
+    A, O, E = _assemble(zs, rA.shape, rO.shape)
+    assert rel(A, rA) < 1e-8 and rel(O, rO) < 1e-9 and rel(E, rE) < 1e-9
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("name", ["g17x16x20_r8", "g12x10x8_r2_stop"])
+def test_library_schedule_world2_matches_golden(tmp_path, name):
+    g = load_golden(name)
+    zs = _run(tmp_path, 2, dict(kind="admm", golden=name))
+    for z in zs:
+        assert int(z["k"]) == g["k"]
+        np.testing.assert_allclose(z["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
+        assert rel(z["B"], g["B"]) < 1e-8 and rel(z["C"], g["C"]) < 1e-8
+    A, O, E = _assemble(zs, g["A"].shape, g["O"].shape)
+    assert rel(A, g["A"]) < 1e-8 and rel(O, g["O"]) < 1e-9 and rel(E, g["E"]) < 1e-9
+
+
+@pytest.mark.timeout(240)
+def test_als_library_schedule_world2_matches_golden(tmp_path):
+    name = "als20x24x18_r5_stop"
+    g = load_golden(name)
+    zs = _run(tmp_path, 2, dict(kind="als", golden=name))
+    for z in zs:
+        assert int(z["k"]) == g["k"]
+        np.testing.assert_allclose(z["errHist"], g["errHist"], rtol=1e-9, atol=1e-14)
+        assert rel(z["B"], g["B"]) < 1e-8 and rel(z["C"], g["C"]) < 1e-8
+    A, _, _ = _assemble(zs, g["A"].shape)
+    assert rel(A, g["A"]) < 1e-8

@@ -1,12 +1,13 @@
 """Print one iteration's kernel sequence (start offset, duration, gap to the
 previous kernel's end) from a rocprofv3 kernel_trace.csv.
-usage: python tools/trace_iter.py TRACE.csv [iteration_index_from_end]"""
+usage: python tools/trace_iter.py TRACE.csv [iteration_index_from_end] [k5_kernel_substring]"""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-k5 = [i for i, r in enumerate(rows) if "k5_fused<" in r["Kernel_Name"] and "true, false" not in r["Kernel_Name"]]
+k5name = sys.argv[3] if len(sys.argv) > 3 else "k5_fused<"
+k5 = [i for i, r in enumerate(rows) if k5name in r["Kernel_Name"] and "true, false" not in r["Kernel_Name"]]
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 a, b = k5[-back - 1], k5[-back]
 t0 = int(rows[a]["End_Timestamp"])

@@ -123,11 +123,8 @@ void AlsSession::set_norm_from_red0() {
 }
 
 void AlsSession::allreduce(double* buf, int64_t count) {
-    if (!comm_ || !comm_->comm) return;
-    const ncclResult_t r =
-        ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, comm_->comm, st_);
-    if (r != ncclSuccess)
-        throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    if (!comm_ || !comm_->active()) return;
+    comm_allreduce(comm_, buf, count, false, st_);
 }
 
 int AlsSession::next_iter() {

@@ -586,6 +586,23 @@ tritd_status tritd_comm_create(tritd_comm** out, const void* id128, int32_t nran
     });
 }
 
+tritd_status tritd_comm_create_host(tritd_comm** out, tritd_allreduce_fn fn, void* user,
+                                    int32_t nranks, int32_t rank, int32_t device) {
+    return guarded([&] {
+        need(out, "out");
+        *out = nullptr;
+        if (!fn) throw Error(TRITD_ERR_ARG, "fn is NULL");
+        if (nranks < 1 || rank < 0 || rank >= nranks) throw Error(TRITD_ERR_ARG, "bad rank/nranks");
+        auto c = std::make_unique<tritd_comm>();
+        c->nranks = nranks;
+        c->rank = rank;
+        c->device = pick_device(device);
+        c->host_fn = fn;
+        c->host_user = user;
+        *out = c.release();
+    });
+}
+
 void tritd_comm_destroy(tritd_comm* c) {
     if (!c) return;
     if (c->comm) (void)ncclCommDestroy(c->comm);

@@ -27,6 +27,11 @@
 #ifndef K5F_EXP
 #define K5F_EXP 0
 #endif
+// k5_f32s: 0 both waves of a pair run the elementwise chain, 1 only one does,
+// 2 = 1 with the roles alternating between workgroups
+#ifndef K5F_LEAN
+#define K5F_LEAN 0
+#endif
 
 namespace tritd {
 
@@ -525,21 +530,28 @@ void k5_f32s(K5Args32 a) {
         }
 #pragma unroll
         for (int m = 0; m < MTH; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        // LEAN: only the h = 0 wave of the pair loads the tile, decodes E and
+        // runs the elementwise chain; the h = 1 wave takes T from the LDS
+        // transpose buffer after one more barrier (its SIMD runs the other
+        // resident wave meanwhile)
+        constexpr bool CHAIN = !K5F_LEAN || h == 0;
         auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
             const int64_t tb = tbase(tt);
             const int64_t o = (tb >> 2) + lane;
             if (pf) {
-                const bool dn1 = ce32_is_dense(nx.ce);
+                const bool dn1 = CHAIN ? ce32_is_dense(nx.ce) : false;
                 stage_load(tt + 1);
-                load(tt + 1, nx);
+                if (CHAIN) load(tt + 1, nx);
                 __builtin_amdgcn_sched_barrier(0);
-                if (dn1) load_dense(tt + 1, nx);
+                if (CHAIN && dn1) load_dense(tt + 1, nx);
             }
-            float ev[4];
-            const bool dn = ce32_decode(cx.ce, lane, ev);
+            float ev[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (CHAIN) {
+                const bool dn = ce32_decode(cx.ce, lane, ev);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
-            if (pf) load_slot(tt + 2, cx.ce);
+                for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
+                if (pf) load_slot(tt + 2, cx.ce);
+            }
             const float* cR = sC[buf];
             f4 lacc[4];
 #pragma unroll
@@ -558,7 +570,7 @@ void k5_f32s(K5Args32 a) {
             float En[4], tr[4];
             f4 YLn, YOn;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < 4 && CHAIN; ++r) {
                 const float d = cx.x[0][r], yl = cx.x[1][r], yo = cx.x[2][r], e = ev[r];
                 const float L = Lv[r];
                 const float R1 = (d - L) + sc.invL * yl;               // :41
@@ -593,6 +605,12 @@ void k5_f32s(K5Args32 a) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) tv[s] = ts[il * 17 + 4 * s + tg];
                 T4[o] = tv;
+            }
+            if (K5F_LEAN) {
+                __syncthreads();  // T of this tile in ts (h = 0 wrote it above)
+                if (h == 1)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) tr[r] = ts[(4 * tg + r) * 17 + il];
             }
             // this half's W M-tiles: granules q in [h*GH, (h+1)*GH)
 #pragma unroll
@@ -644,7 +662,11 @@ void k5_f32s(K5Args32 a) {
                 wl[slot * WS + k * 16 + il] = wacc[mq][rr];
             }
     };
-    if (wid & 1)
+    // the pair's roles alternate between workgroups (LEAN: the h = 0 wave
+    // carries the elementwise chain; the two workgroups resident on a CU then
+    // put it on different SIMDs, as far as waves map to SIMDs in order)
+    const int hrole = (wid & 1) ^ ((K5F_LEAN > 1) ? (int)(blockIdx.x & 1) : 0);
+    if (hrole)
         walk(std::integral_constant<int, 1>{});
     else
         walk(std::integral_constant<int, 0>{});
@@ -663,7 +685,7 @@ void k5_f32s(K5Args32 a) {
             if (ok) dst[(int64_t)k * a.plane] = wl[sl * WS + k * 16 + il];
         }
     }
-    if ((wid & 1) == 0 && ndense && lane == 0)
+    if (hrole == 0 && ndense && lane == 0)
         atomicAdd(a.dense_tiles + ((blockIdx.x * 2 + slot) & (DENSE_SLOTS - 1)), (unsigned long long)ndense);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -672,13 +694,13 @@ void k5_f32s(K5Args32 a) {
     }
     __shared__ double red[2][4];
     if (lane == 0) {
-        red[0][wid] = ssL;  // 0 for the odd waves
+        red[0][wid] = ssL;  // exactly 0 for the h = 1 waves
         red[1][wid] = ssO;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        a.partial[2 * blockIdx.x] = red[0][0] + red[0][2];
-        a.partial[2 * blockIdx.x + 1] = red[1][0] + red[1][2];
+    if (threadIdx.x == 0) {  // adding the h = 1 zeros is exact: the pair sum of the h = 0 waves
+        a.partial[2 * blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        a.partial[2 * blockIdx.x + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
     }
 }
 

@@ -5,6 +5,8 @@
 // accumulated in single here (W and T are single); the factor operands
 // (A^ o B^, B^, A^) are the double factors rounded to single, as MATLAB
 // converts the double design matrix F/G/H when it meets a single X_k.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace tritd {
@@ -261,10 +263,88 @@ __global__ __launch_bounds__(256) void k_apply_gen(const TM* __restrict__ M, int
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same product on f64 MFMA (the default): one wave per 16 x 16 tile of Y,
+// A[m][k] = M(r0+m, 4s+k), B[k][n] = Ginv(4s+k, 16ct+n), RP/4 K-steps whose
+// operands are loaded in batches of 16 before their MFMAs (both inputs are
+// L2-resident: M is rows x RP, Ginv RP x RP).  At config 5 (rows 2048,
+// RP 256) k_apply_gen took 0.28 ms per apply, three per iteration on the
+// critical path (128 workgroups of sequential dot products).
+// ---------------------------------------------------------------------------
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <int RP, typename TM>
+__global__ __launch_bounds__(256) void k_apply_mfma(const TM* __restrict__ M, int64_t rows,
+                                                    const double* __restrict__ Ginv, double* Y,
+                                                    double* YT, int64_t ldT, float* YF,
+                                                    int round32, const int* stop) {
+    if (stop && *stop) return;
+    constexpr int NT = RP / 16, KS = RP / 4, BATCH = KS < 16 ? KS : 16;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
+    const int64_t rt = tile / NT;
+    const int ct = (int)(tile - rt * NT);
+    const int64_t r0 = rt * 16;
+    if (r0 >= rows) return;  // wave-uniform
+    const int m = lane & 15, kq = lane >> 4;
+    const bool in = r0 + m < rows;
+    const TM* mp = M + (in ? (r0 + m) * RP : 0) + kq;
+    const double* gp = Ginv + (int64_t)kq * RP + 16 * ct + m;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s0 = 0; s0 < KS; s0 += BATCH) {
+        double a[BATCH], b[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            a[u] = in ? (double)mp[4 * (s0 + u)] : 0.0;
+            b[u] = gp[(int64_t)4 * (s0 + u) * RP];
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+    }
+    const int k = 16 * ct + m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i = r0 + kq + 4 * r;
+        if (i >= rows) continue;
+        double v = acc[r];
+        if (round32) v = (double)(float)v;
+        Y[i * RP + k] = v;
+        if (YT) YT[(int64_t)k * ldT + i] = v;
+        if (YF) YF[i * RP + k] = (float)v;
+    }
+}
+
 void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, double* Ginv,
                       double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
                       int* flags, hipStream_t st) {
     launch_pinv_fix(RP, Ginv, stop, flags, st);
+    static const bool old = std::getenv("TRITD_APPLY_GEN") != nullptr;  // A/B: the VALU kernel
+    if (!old) {
+        const int64_t tiles = cdiv(rows, 16) * (RP / 16);
+        const dim3 grid((unsigned)cdiv(tiles, 4)), block(256);
+#define APPLY_MF_CASE(RPV)                                                                          \
+    case RPV:                                                                                       \
+        if (Mf)                                                                                     \
+            hipLaunchKernelGGL((k_apply_mfma<RPV, float>), grid, block, 0, st, Mf, rows, Ginv, Y, YT, \
+                               ldT, YF, (int)round32, stop);                                        \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_apply_mfma<RPV, double>), grid, block, 0, st, M, rows, Ginv, Y,   \
+                               YT, ldT, YF, (int)round32, stop);                                    \
+        break;
+        switch (RP) {
+            APPLY_MF_CASE(16)
+            APPLY_MF_CASE(32)
+            APPLY_MF_CASE(48)
+            APPLY_MF_CASE(64)
+            APPLY_MF_CASE(128)
+            APPLY_MF_CASE(256)
+            default: throw Error(TRITD_ERR_UNSUPPORTED, "apply: RP not supported");
+        }
+#undef APPLY_MF_CASE
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     const size_t lds = (size_t)16 * (RP + 1) * sizeof(double);
     const dim3 grid((unsigned)cdiv(rows, 16)), block(256);
     if (Mf)

@@ -103,7 +103,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         const char* gms = std::getenv("TRITD_GRAM_MAIN_SH");  // sharded schedule
         gram_main_sh_ = gms ? std::atoi(gms) : 0;
         const char* sh = std::getenv("TRITD_SHOV");
-        shov_ = comm != nullptr && comm->comm != nullptr && shared_stream == nullptr &&
+        shov_ = comm != nullptr && comm->active() && shared_stream == nullptr &&
                 !(sh && std::atoi(sh) == 0);
     }
     create_streams(shared_stream);
@@ -196,7 +196,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         for (DBuf* b : {&GqA_, &GqB_, &GqC_}) b->alloc((size_t)g_.RP * g_.RP);
     }
     k5tail_ = k5n();
-    if (comm_ && comm_->comm) agree_counts();
+    if (comm_ && comm_->active()) agree_counts();
     red1_.alloc(red1_count() + 2 * (size_t)k5tail_);  // + the tail for K5's norm partials
     red2_.alloc(red2_count());
     red3_.alloc(2);
@@ -472,11 +472,25 @@ void Session::launch_k5_any(int k, bool prologue) {
     launch_k5(g_, a, prologue, dy_, st_);
 }
 
+void comm_allreduce(tritd_comm* c, double* buf, int64_t count, bool max, hipStream_t st) {
+    if (c->comm) {
+        const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64,
+                                             max ? ncclMax : ncclSum, c->comm, st);
+        if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        return;
+    }
+    std::vector<double> h((size_t)count);
+    TRITD_HIP(hipMemcpyAsync(h.data(), buf, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    TRITD_HIP(hipStreamSynchronize(st));
+    if (c->host_fn(h.data(), count, max ? 1 : 0, c->host_user) != 0)
+        throw Error(TRITD_ERR_RCCL, "host all-reduce callback failed");
+    TRITD_HIP(hipMemcpyAsync(buf, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    TRITD_HIP(hipStreamSynchronize(st));
+}
+
 void Session::allreduce(double* buf, int64_t count) {
-    if (!comm_ || !comm_->comm) return;
-    const ncclResult_t r =
-        ncclAllReduce(buf, buf, (size_t)count, ncclFloat64, ncclSum, comm_->comm, st_);
-    if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    if (!comm_ || !comm_->active()) return;
+    comm_allreduce(comm_, buf, count, false, st_);
 }
 
 // Every rank must issue each all-reduce with the same count.  red1 and red2
@@ -498,8 +512,7 @@ void Session::agree_counts() {
     DBuf v;
     v.alloc(10);
     TRITD_HIP(hipMemcpyAsync(v.p, h, sizeof h, hipMemcpyHostToDevice, st_));
-    const ncclResult_t r = ncclAllReduce(v.p, v.p, 10, ncclFloat64, ncclMax, comm_->comm, st_);
-    if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    comm_allreduce(comm_, v.p, 10, /*max=*/true, st_);
     TRITD_HIP(hipMemcpyAsync(h, v.p, sizeof h, hipMemcpyDeviceToHost, st_));
     TRITD_HIP(hipStreamSynchronize(st_));
     k5tail_ = (int)h[0];
@@ -756,7 +769,7 @@ void Session::iterate_fused(int k) {
     do_m1();
     do_apply_A(GinvA_.p);
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
-    if (comm_ && comm_->comm) {
+    if (comm_ && comm_->active()) {
         do_m2(M2);
         // M1 .. M2 above ran before the stop test of iteration k-1: they
         // write only scratch and this iteration's A^ parity buffer.  The
@@ -792,7 +805,7 @@ void Session::iterate_fused(int k) {
     // the next update_A's solve (B^TB, C^TC of this iteration) beside K5
     k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;
     k5side_.flags = ctrl_ + 2; k5side_.R = g_.R; k5side_.on = 1;
-    if (comm_ && comm_->comm) {
+    if (comm_ && comm_->active()) {
         // the norm partials stay per workgroup in red1_'s tail: all-reduced
         // with the next iteration's M2 | A^TA (or by flush_norms)
         k5part_to_ = red1_.p + red1_count();

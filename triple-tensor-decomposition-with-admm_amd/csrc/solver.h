@@ -8,11 +8,18 @@
 #include "kernels.h"
 
 struct tritd_comm {
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;             // RCCL (tritd_comm_create)
+    tritd_allreduce_fn host_fn = nullptr;  // or a host transport (tritd_comm_create_host)
+    void* host_user = nullptr;
     int nranks = 1, rank = 0, device = 0;
+    bool active() const { return comm != nullptr || host_fn != nullptr; }
 };
 
 namespace tritd {
+
+// In-place all-reduce (sum, or max) of `count` doubles over the comm's ranks,
+// ordered on stream st: ncclAllReduce, or the host transport (drains st).
+void comm_allreduce(tritd_comm* c, double* buf, int64_t count, bool max, hipStream_t st);
 
 // A device buffer of doubles; freed on destruction.
 struct DBuf {

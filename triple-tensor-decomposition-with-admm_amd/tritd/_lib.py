@@ -48,6 +48,8 @@ class Opts(C.Structure):
 
 
 PRINT_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
+# tritd_allreduce_fn: (buf, count, op 0 sum / 1 max, user) -> 0 on success
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int32, C.POINTER(C.c_double), C.c_int64, C.c_int32, C.c_void_p)
 
 dp = C.POINTER(C.c_double)
 vp = C.c_void_p
@@ -83,6 +85,7 @@ SIGNATURES = {
     "tritd_session_destroy": (None, [vp]),
     "tritd_comm_unique_id": (C.c_int, [vp]),
     "tritd_comm_create": (C.c_int, [C.POINTER(vp), vp, i32, i32, i32]),
+    "tritd_comm_create_host": (C.c_int, [C.POINTER(vp), ALLREDUCE_FN, vp, i32, i32, i32]),
     "tritd_comm_destroy": (None, [vp]),
     "tritd_admm_sharded_virtual_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp,
                                                  vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32),

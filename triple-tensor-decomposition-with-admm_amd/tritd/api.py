@@ -577,12 +577,38 @@ class AlsSession:
 
 
 class Comm:
-    """RCCL communicator owned by libtritd (one process per GPU)."""
+    """RCCL communicator owned by libtritd (one process per GPU), or — with
+    :meth:`host` — a host transport that hands every all-reduce to a Python
+    function (tritd_comm_create_host)."""
 
     def __init__(self, unique_id: bytes, nranks, rank, device):
         self.handle = C.c_void_p()
         buf = C.create_string_buffer(bytes(unique_id), 128)
         check(lib.tritd_comm_create(C.byref(self.handle), buf, int(nranks), int(rank), int(device)))
+
+    @classmethod
+    def host(cls, fn, nranks, rank, device):
+        """fn(buf, op) all-reduces the float64 numpy array `buf` in place over
+        the ranks (op 0: sum, 1: max).  Every all-reduce of a session drains
+        its stream first: a correctness transport (several ranks on one GPU,
+        hosts with their own collectives), not the fast path."""
+        self = cls.__new__(cls)
+        self.handle = C.c_void_p()
+
+        def cb(buf, count, op, user):
+            try:
+                if count > 0:
+                    fn(np.ctypeslib.as_array(buf, shape=(int(count),)), int(op))
+                return 0
+            except Exception:  # reported to the library as a failed collective
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._cb = _lib.ALLREDUCE_FN(cb)  # kept alive with the comm
+        check(lib.tritd_comm_create_host(C.byref(self.handle), self._cb, None, int(nranks),
+                                         int(rank), int(device)))
+        return self
 
     @staticmethod
     def unique_id() -> bytes:

@@ -37,3 +37,17 @@ def make_comm(torch_dist, rank: int, world: int, device: int):
     uid = [Comm.unique_id() if rank == 0 else None]
     torch_dist.broadcast_object_list(uid, src=0)
     return Comm(uid[0], world, rank, device)
+
+
+def make_host_comm(torch_dist, rank: int, world: int, device: int):
+    """libtritd communicator whose all-reduces go through torch.distributed on
+    host copies (any backend, e.g. gloo): the library's own multi-rank
+    schedule with several ranks on one GPU, where RCCL cannot run."""
+    import torch
+    from .api import Comm
+
+    def fn(buf, op):
+        t = torch.from_numpy(buf)  # shares memory: the reduced values land in buf
+        torch_dist.all_reduce(t, op=torch_dist.ReduceOp.MAX if op else torch_dist.ReduceOp.SUM)
+
+    return Comm.host(fn, world, rank, device)

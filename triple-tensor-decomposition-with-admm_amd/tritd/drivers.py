@@ -94,15 +94,19 @@ def video_triple(X, r=5, missing_ratio=0.0, *, opts=None, seed=0, A0=None, B0=No
     `triple_decomp_ADMM_outlier` name the script calls (:54): RMSE/NRMSE of
     X_hat on the missing entries, of O on the observed ones, of X_hat + O on
     all of them, and PSNR/SSIM of X_hat against X (quality_ybz), printed as at
-    :74-75.  With `save_dir` (and missing_ratio == plot_rate == 0, :58) the
-    errHist / X_hat / O .mat files of :59-61 are written."""
+    :74-75.  With `save_dir` the observed tensor is saved as `<name>_raw.mat`
+    (variable Y, :32, every ratio) and, when missing_ratio == plot_rate == 0
+    (:58), the errHist / X_hat / O .mat files of :59-61."""
     X = np.asfortranarray(np.asarray(X, dtype=np.float64))
     rng = np.random.default_rng(seed)
     mask = missing_mask(X.shape, missing_ratio, rng)
     printer("\n===== Dataset: %s Missing Radio %.3f=====" % (name, missing_ratio))
     Y = _observe(X, mask)
-    gt = X.ravel(order="F")[mask.ravel(order="F")]       # X(mask_missing), column-major (:32)
-    gt_2 = X.ravel(order="F")[~mask.ravel(order="F")]    # X(~mask_missing)              (:33)
+    if save_dir is not None:  # save(sprintf("%s_raw.mat", name), 'Y')  (:32)
+        from scipy.io import savemat
+        savemat(os.path.join(save_dir, "%s_raw.mat" % name), {"Y": Y})
+    gt = X.ravel(order="F")[mask.ravel(order="F")]       # X(mask_missing), column-major (:36)
+    gt_2 = X.ravel(order="F")[~mask.ravel(order="F")]    # X(~mask_missing)              (:37)
     o = dict(VIDEO_OPTS if opts is None else opts)
     t0 = time.perf_counter()
     A, B, C, O, errHist = api.triple_decomp_ADMM_outlier(Y, r, o, A0, B0, C0)
