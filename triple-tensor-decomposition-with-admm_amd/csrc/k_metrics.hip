@@ -165,13 +165,38 @@ __global__ __launch_bounds__(EV_THREADS) void k_eval_full(const double* __restri
                                                           int64_t n, double* __restrict__ part) {
     const int64_t base = (int64_t)blockIdx.x * EV_CHUNK;
     double sd = 0.0, sg = 0.0;
-    for (int q = 0; q < EV_ROUNDS; ++q) {
-        const int64_t e = base + (int64_t)q * EV_THREADS + threadIdx.x;
-        if (e < n) {
-            const double g = gt[e];
-            const double d = X[e] - g;
-            sd += d * d;
-            sg += g * g;
+    const bool whole = base + EV_CHUNK <= n && (((uintptr_t)X | (uintptr_t)gt) & 15) == 0;
+    if (whole) {
+        // every block but the last: 16-byte nontemporal loads, all issued before
+        // the arithmetic (round 5: the tensors are streamed once)
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        constexpr int Q = EV_ROUNDS / 2;
+        const d2* X2 = reinterpret_cast<const d2*>(X + base);
+        const d2* G2 = reinterpret_cast<const d2*>(gt + base);
+        d2 xv[Q], gv[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            xv[q] = __builtin_nontemporal_load(X2 + q * EV_THREADS + threadIdx.x);
+            gv[q] = __builtin_nontemporal_load(G2 + q * EV_THREADS + threadIdx.x);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const double d = xv[q][c] - gv[q][c];
+                sd += d * d;
+                sg += gv[q][c] * gv[q][c];
+            }
+        }
+    } else {
+        for (int q = 0; q < EV_ROUNDS; ++q) {
+            const int64_t e = base + (int64_t)q * EV_THREADS + threadIdx.x;
+            if (e < n) {
+                const double g = gt[e];
+                const double d = X[e] - g;
+                sd += d * d;
+                sg += g * g;
+            }
         }
     }
     __shared__ double sh[EV_THREADS / 64];

@@ -212,7 +212,9 @@ void launch_pack_factors(const Geom& g, const double* A, const double* B, const 
 // K0: batched transpose in[b][c][r] (r fastest) -> out[b][r][c] (c fastest).
 //   unfold mode 2 (permute [2 1 3]): rows n1, cols n2, batch n3
 //   unfold mode 3 (permute [3 1 2]): rows n1*n2, cols n3, batch 1
-// 64 x 64 tile through LDS, 16-byte global accesses on both sides.
+// 64 x 64 tile through LDS, 16-byte global accesses on both sides, nontemporal
+// (streamed once: round 5, tools/unfold3_probe.hip at 512^3, mode 2 0.352 ->
+// 0.329 ms = 6.52 TB/s).
 // ---------------------------------------------------------------------------
 constexpr int TT = 64;
 // FULL: every tile is whole and 16-B aligned (checked on the host), so the
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in
             d2v v[8];
 #pragma unroll
             for (int m = 0; m < 8; ++m)
-                v[m] = *reinterpret_cast<const d2v*>(src + (c0 + cc + 8 * m) * rows + r0 + rr);
+                v[m] = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src + (c0 + cc + 8 * m) * rows + r0 + rr));
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 tile[cc + 8 * m][rr] = v[m].x;
@@ -260,7 +262,8 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in
             const int r = rr + 8 * m;
             const int64_t gr = r0 + r, gc = c0 + cc;
             if constexpr (FULL) {
-                *reinterpret_cast<d2v*>(dst + gr * cols + gc) = d2v{tile[cc][r], tile[cc + 1][r]};
+                __builtin_nontemporal_store(d2v{tile[cc][r], tile[cc + 1][r]},
+                                            reinterpret_cast<d2v*>(dst + gr * cols + gc));
             } else {
                 if (gr < rows && gc < cols) dst[gr * cols + gc] = tile[cc][r];
                 if (gr < rows && gc + 1 < cols) dst[gr * cols + gc + 1] = tile[cc + 1][r];
@@ -275,6 +278,9 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ in
 // of rows spread over the whole output, and all global loads issue before
 // the LDS stores.  Measured at 512^3 (tools/prim_stream.hip): 32 x 128 tiles
 // 0.385 ms = 5.58 TB/s vs 0.41 ms for the 64 x 64 row-fastest kernel.
+// Round 5 (tools/unfold3_probe.hip, one box): nontemporal loads and stores
+// and 128 x 64 tiles (1 KB read runs per column) 0.337 ms = 6.38 TB/s; 32 x
+// 128 nontemporal 0.347, plain 0.369.
 template <int TR, int TC>
 __global__ __launch_bounds__(256) void k_transpose_tall(const double* __restrict__ in,
                                                         double* __restrict__ out, int64_t rows,
@@ -288,7 +294,8 @@ __global__ __launch_bounds__(256) void k_transpose_tall(const double* __restrict
     const int rp = th % PR, cc = th / PR;
 #pragma unroll
     for (int m = 0; m < ML; ++m)
-        v[m] = *reinterpret_cast<const d2v*>(in + (c0 + cc + CPP * m) * rows + r0 + 2 * rp);
+        v[m] = __builtin_nontemporal_load(
+            reinterpret_cast<const d2v*>(in + (c0 + cc + CPP * m) * rows + r0 + 2 * rp));
 #pragma unroll
     for (int m = 0; m < ML; ++m) {
         tile[cc + CPP * m][2 * rp] = v[m].x;
@@ -300,8 +307,8 @@ __global__ __launch_bounds__(256) void k_transpose_tall(const double* __restrict
 #pragma unroll
     for (int m = 0; m < MS; ++m) {
         const int r = rr + RPP * m;
-        *reinterpret_cast<d2v*>(out + (r0 + r) * cols + c0 + 2 * cp) =
-            d2v{tile[2 * cp][r], tile[2 * cp + 1][r]};
+        __builtin_nontemporal_store(d2v{tile[2 * cp][r], tile[2 * cp + 1][r]},
+                                    reinterpret_cast<d2v*>(out + (r0 + r) * cols + c0 + 2 * cp));
     }
 }
 
@@ -316,7 +323,7 @@ void launch_transpose_batched(const double* in, double* out, int64_t rows, int64
     }
     if (cdiv(rows, TT) > INT32_MAX || cdiv(cols, TT) > 65535)
         throw Error(TRITD_ERR_ARG, "unfold: matrix too large for one transpose launch");
-    constexpr int TR = 32, TC = 128;
+    constexpr int TR = 128, TC = 64;
     if (batch == 1 && rows % TR == 0 && cols % TC == 0 && rows >= 64 * cols &&
         (((uintptr_t)in | (uintptr_t)out) & 15) == 0 && (rows / TR) * (cols / TC) < (1LL << 31)) {
         const int64_t nct = cols / TC;
