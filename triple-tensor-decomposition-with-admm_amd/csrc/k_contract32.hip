@@ -48,10 +48,67 @@ __global__ __launch_bounds__(256) void k_m1_32(const float* __restrict__ Wk,
     if (w == 0 && i < n1p) M1[i * RP + k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
+// Round 5: 16-byte loads (a lane owns 4 consecutive i, a wave 1 KB of a
+// j-row), U = 8 rows in flight per wave; the 4 waves take every 4th j and are
+// summed through LDS in fixed order.  W at config 5 is 4.3 GB (as big as
+// the tensor) and is read by M1 and M2: the 4-byte kernels above read it at
+// ~4 TB/s (1.06 / 1.24 ms per launch).
+__global__ __launch_bounds__(256) void k_m1_32v(const float* __restrict__ Wk,
+                                                const double* __restrict__ Bh, float* M1,
+                                                int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                                const int* stop) {
+    if (*stop) return;
+    constexpr int U = 8;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 256 + 4 * lane;
+    const int k = blockIdx.y;
+    const bool in = i < n1p;  // n1p % 16 == 0: i..i+3 all in range
+    f4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    const f4* wp = reinterpret_cast<const f4*>(Wk + (int64_t)k * plane + (in ? i : 0));
+    const int64_t ld4 = n1p >> 2;
+    const double* bp = Bh + k;
+    int64_t j = w;
+    for (; j + 4 * (U - 1) < n2; j += 4 * U) {
+        f4 v[U];
+        float b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = in ? __builtin_nontemporal_load(wp + (j + 4 * u) * ld4) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+            b[u] = (float)bp[(j + 4 * u) * RP];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[u][c] = fmaf(v[u][c], b[u], acc[u][c]);
+    }
+    for (; j < n2; j += 4) {
+        const f4 v = in ? wp[j * ld4] : f4{0.0f, 0.0f, 0.0f, 0.0f};
+        const float b = (float)bp[j * RP];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[0][c] = fmaf(v[c], b, acc[0][c]);
+    }
+    f4 t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __shared__ f4 red[4][64];
+    red[w][lane] = t;
+    __syncthreads();
+    if (w == 0 && in) {
+        const f4 sum = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) M1[(i + c) * RP + k] = sum[c];
+    }
+}
+
 void launch_m1_32(const Geom& g, const float* Wk, const double* Bh, float* M1, const int* stop,
                   hipStream_t st) {
-    hipLaunchKernelGGL(k_m1_32, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(256), 0, st, Wk, Bh,
-                       M1, g.n1p, g.n2, g.plane, g.RP, stop);
+    static const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;  // A/B: the 4-byte kernels
+    if (!old)
+        hipLaunchKernelGGL(k_m1_32v, dim3((unsigned)cdiv(g.n1p, 256), g.RP), dim3(256), 0, st, Wk, Bh,
+                           M1, g.n1p, g.n2, g.plane, g.RP, stop);
+    else
+        hipLaunchKernelGGL(k_m1_32, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(256), 0, st, Wk, Bh,
+                           M1, g.n1p, g.n2, g.plane, g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -76,10 +133,62 @@ __global__ __launch_bounds__(256) void k_m2_32(const float* __restrict__ Wk,
     if (lane == 0) M2[j * RP + k] = (double)acc;
 }
 
+// Round 5: 16-byte loads, a lane 4 consecutive i per step, four independent
+// accumulators, every load of the row in flight before the sums (n1p/256
+// steps per wave; 8 at config 5).
+__global__ __launch_bounds__(256) void k_m2_32v(const float* __restrict__ Wk,
+                                                const double* __restrict__ AhT, double* M2,
+                                                int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                                const int* stop) {
+    if (*stop) return;
+    constexpr int U = 8;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t j = blockIdx.x;
+    const int k = blockIdx.y * 4 + w;
+    if (k >= RP) return;
+    const f4* wp = reinterpret_cast<const f4*>(Wk + (int64_t)k * plane + j * n1p);
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2* ap = reinterpret_cast<const d2*>(AhT + (int64_t)k * n1p);
+    const int64_t n4 = n1p >> 2;  // float4 groups of the row
+    f4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int64_t g0 = lane; g0 < n4; g0 += 64 * U) {
+        f4 v[U];
+        d2 a0[U], a1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t g = g0 + 64 * u;
+            const bool in = g < n4;
+            v[u] = in ? __builtin_nontemporal_load(wp + g) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+            a0[u] = in ? ap[2 * g] : d2{0.0, 0.0};
+            a1[u] = in ? ap[2 * g + 1] : d2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            f4& ac = acc[u & 3];
+            ac[0] = fmaf(v[u][0], (float)a0[u][0], ac[0]);
+            ac[1] = fmaf(v[u][1], (float)a0[u][1], ac[1]);
+            ac[2] = fmaf(v[u][2], (float)a1[u][0], ac[2]);
+            ac[3] = fmaf(v[u][3], (float)a1[u][1], ac[3]);
+        }
+    }
+    const f4 t4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    float acc1 = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc1 += __shfl_xor(acc1, off);
+    if (lane == 0) M2[j * RP + k] = (double)acc1;
+}
+
 void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
                   hipStream_t st) {
-    hipLaunchKernelGGL(k_m2_32, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
-                       AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
+    static const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;
+    if (!old)
+        hipLaunchKernelGGL(k_m2_32v, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
+                           AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
+    else
+        hipLaunchKernelGGL(k_m2_32, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
+                           AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 
