@@ -203,3 +203,24 @@ def test_sharded_als_world2_matches_golden(tmp_path, name):
         assert rel(z["B"], g["B"]) < 1e-8 and rel(z["C"], g["C"]) < 1e-8
         np.testing.assert_allclose(z["errHist"], g["errHist"], rtol=1e-9, atol=1e-14)
     assert rel(A, g["A"]) < 1e-8
+
+
+def test_allreduce_counts_agree_for_every_partition():
+    """Every shard_bounds partition (n1 <= 200, 1..8 ranks) gives every rank the
+    same all-reduce counts once red1's norm tail is sized to the largest
+    shard's K5 grid (solver.cpp agree_counts), although the per-rank grids
+    differ whenever the padded shard heights straddle a multiple of 16."""
+    import tritd_sharded
+    from tritd.dist import all_bounds
+    n2, n3, RP = 10, 8, 16
+    straddles = 0
+    for n1 in range(1, 201):
+        for world in range(1, 9):
+            if world > n1:
+                continue
+            grids = [tritd_sharded.k5_workgroups(i1 - i0, n2) for i0, i1 in all_bounds(n1, world)]
+            tail = max(grids)
+            counts = {(n2 * RP + RP * RP + 2 * tail, ((n3 + 15) // 16 * 16) * RP) for _ in grids}
+            assert len(counts) == 1
+            straddles += len(set(grids)) > 1
+    assert straddles > 0  # the max is needed: some partitions give the ranks different grids
