@@ -55,6 +55,18 @@ __device__ double work(int iters, double seed) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[q]) : "v"(x[(q + 1) & 7]));
         for (int q = 0; q < 8; ++q) out += x[q];
+    } else if (ROLE == 7) {
+        // v_mfma_f32_16x16x4_f32, 4 independent accumulators (config 5's K5/K2)
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        f4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+        float a = (float)seed, b = (float)seed * 0.5f;
+        for (int i = 0; i < iters * 2; ++i) {
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, c1, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, c2, 0, 0, 0);
+            c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, c3, 0, 0, 0);
+        }
+        out = c0[0] + c1[1] + c2[2] + c3[3];
     } else if (ROLE == 4) {
         float x[8];
         for (int q = 0; q < 8; ++q) x[q] = (float)seed + q;
@@ -104,5 +116,10 @@ int main() {
     run(k_co<0, 6>, "idle | cndmask");
     run(k_co<1, 6>, "mfma | cndmask");
     run(k_co<3, 3>, "int | int");
+    run(k_co<7, 0>, "mfma32 | idle");
+    run(k_co<7, 4>, "mfma32 | fma_f32");
+    run(k_co<7, 3>, "mfma32 | int");
+    run(k_co<7, 2>, "mfma32 | fma_f64");
+    run(k_co<7, 7>, "mfma32 | mfma32");
     return 0;
 }

@@ -15,3 +15,5 @@ bash tools/refresh_profiles_c5.sh r05 > gpurun_out/refresh_c5.log 2>&1 || exit $
 tail -1 gpurun_out/refresh_c5.log | cut -c1-400
 timeout -k 10 300 python3 bench.py --algo als --steps 20 --warmup 3 > gpurun_out/bench_als.json 2> gpurun_out/bench_als.err || exit $?
 cut -c1-300 gpurun_out/bench_als.json
+timeout -k 10 60 tools/coexec > gpurun_out/coexec.log 2>&1 || exit $?
+cat gpurun_out/coexec.log

@@ -214,7 +214,11 @@ static int64_t m3_jchunks(const Geom& g) {
 
 int m3_parts32(const Geom& g) { return (int)((g.n1p >> 4) * m3_jchunks(g)); }
 
-template <int RP>
+// V (RP >= 64, the default there): KR stored [ij][il][m] with a 4-float pad
+// per (ij, il) row (pitch MT + 4: the 16 lanes of a quarter-wave start on
+// distinct 4-bank groups), so one ds_read_b128 gives a lane the A operands of
+// four consecutive k-tiles — 4x fewer LDS reads than one float per MFMA.
+template <int RP, bool V>
 __global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
                                                     const double* __restrict__ Ah,
                                                     const double* __restrict__ Bh, double* part,
@@ -235,7 +239,9 @@ __global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
     const bool tact = tt < ntt;
     const int64_t ttl = tact ? tt : ntt - 1;  // inactive waves read a valid tile, store nothing
 
-    __shared__ float krs[2][16 * KP];
+    constexpr int PITCH = MT + 4;  // V layout: [row][il][m], m fastest
+    constexpr int KSZ = V ? 16 * 16 * PITCH : 16 * KP;
+    __shared__ __attribute__((aligned(16))) float krs[2][KSZ];
     // this thread's KR elements: e = threadIdx.x + 256 u -> (row e / RP, col e % RP)
     double ah[PER > 0 ? PER : 1];
 #pragma unroll
@@ -248,7 +254,8 @@ __global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
         for (int u = 0; u < PER; ++u) {
             const int e = threadIdx.x + 64 * M3W * u;
             const int row = e / RP, k = e % RP;
-            krs[buf][row * KP + k] = (float)(ah[u] * Bh[j * RP + k]);
+            const int at = V ? (row * 16 + (k & 15)) * PITCH + (k >> 4) : row * KP + k;
+            krs[buf][at] = (float)(ah[u] * Bh[j * RP + k]);
         }
     };
     f4 acc[MT];
@@ -269,11 +276,24 @@ __global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
                 form(j + 1, buf ^ 1);
             }
             const float* kr = krs[buf];
+            if constexpr (V) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
+                for (int s = 0; s < 4; ++s) {
+                    const f4* ar = reinterpret_cast<const f4*>(kr + ((4 * s + tg) * 16 + il) * PITCH);
 #pragma unroll
-                for (int m = 0; m < MT; ++m)
-                    acc[m] = mfma32c(kr[(4 * s + tg) * KP + 16 * m + il], b[s], acc[m]);
+                    for (int mq = 0; mq < MT / 4; ++mq) {
+                        const f4 a4 = ar[mq];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) acc[4 * mq + u] = mfma32c(a4[u], b[s], acc[4 * mq + u]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int m = 0; m < MT; ++m)
+                        acc[m] = mfma32c(kr[(4 * s + tg) * KP + 16 * m + il], b[s], acc[m]);
+            }
             __syncthreads();
         }
     }
@@ -308,10 +328,15 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
                   double* M3, const int* stop, hipStream_t st) {
     const int64_t jc = m3_jchunks(g), qper = g.n1p >> 4, ntg = cdiv(g.ntt, 4);
     const dim3 grid((unsigned)(ntg * qper * jc)), block(64 * M3W);
-#define M3F_CASE(RPV)                                                                        \
-    case RPV:                                                                                \
-        hipLaunchKernelGGL(k_m3_32<RPV>, grid, block, 0, st, T, Ah, Bh, part, g.n1p, g.n2,   \
-                           g.n3p, g.ntt, jc, stop);                                          \
+    static const bool oldk = std::getenv("TRITD_M3F_OLD") != nullptr;  // A/B: one float per MFMA
+#define M3F_CASE(RPV)                                                                              \
+    case RPV:                                                                                      \
+        if (RPV >= 64 && !oldk)                                                                    \
+            hipLaunchKernelGGL((k_m3_32<RPV, (RPV >= 64)>), grid, block, 0, st, T, Ah, Bh, part,   \
+                               g.n1p, g.n2, g.n3p, g.ntt, jc, stop);                               \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_m3_32<RPV, false>), grid, block, 0, st, T, Ah, Bh, part, g.n1p,  \
+                               g.n2, g.n3p, g.ntt, jc, stop);                                      \
         break;
     switch (g.RP) {
         M3F_CASE(16)
