@@ -26,7 +26,10 @@ opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
 res = {v: [] for v in vals}
 for rep in range(reps):
     for v in vals:
-        os.environ[var] = v
+        if v == "-":  # "-": the variable unset
+            os.environ.pop(var, None)
+        else:
+            os.environ[var] = v
         s = tritd.Session(r, opts, A0, B0, C0, n1=n1, n2=n2, n3=n3, D=D, device=0, dtype=D.dtype)
         s.run(int(os.environ.get('AB_WARM', '15'))); s.sync(); s.set_timing(True); s.run(iters); s.sync()
         km = s.kernel_ms()

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k_m1_32v(const float* __restrict__ Wk,
 
 void launch_m1_32(const Geom& g, const float* Wk, const double* Bh, float* M1, const int* stop,
                   hipStream_t st) {
-    static const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;  // A/B: the 4-byte kernels
+    const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;  // A/B: the 4-byte kernels (per launch)
     if (!old)
         hipLaunchKernelGGL(k_m1_32v, dim3((unsigned)cdiv(g.n1p, 256), g.RP), dim3(256), 0, st, Wk, Bh,
                            M1, g.n1p, g.n2, g.plane, g.RP, stop);
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void k_m2_32v(const float* __restrict__ Wk,
 
 void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
                   hipStream_t st) {
-    static const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;
+    const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;
     if (!old)
         hipLaunchKernelGGL(k_m2_32v, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
                            AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
@@ -328,7 +328,7 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
                   double* M3, const int* stop, hipStream_t st) {
     const int64_t jc = m3_jchunks(g), qper = g.n1p >> 4, ntg = cdiv(g.ntt, 4);
     const dim3 grid((unsigned)(ntg * qper * jc)), block(64 * M3W);
-    static const bool oldk = std::getenv("TRITD_M3F_OLD") != nullptr;  // A/B: one float per MFMA
+    const bool oldk = std::getenv("TRITD_M3F_OLD") != nullptr;  // A/B (read per launch: tools/ab_env.py)
 #define M3F_CASE(RPV)                                                                              \
     case RPV:                                                                                      \
         if (RPV >= 64 && !oldk)                                                                    \
