@@ -46,8 +46,12 @@ def _flat(x):
 def sumsq_diff(a, b, chunk=1 << 24):
     """(sum (a-b)^2, sum b^2) in float64, chunked: full-size tensors (1e9
     elements) without float64 temporaries of their whole size."""
-    a, b = _flat(a), _flat(b)
+    a, b = np.asarray(a), np.asarray(b)
     assert a.shape == b.shape
+    if a.ndim > 1 and not (a.flags.f_contiguous and b.flags.f_contiguous) and \
+            not (a.flags.c_contiguous and b.flags.c_contiguous):
+        a, b = np.asfortranarray(a), np.asfortranarray(b)  # one memory order for both
+    a, b = _flat(a), _flat(b)
     num = den = 0.0
     for s in range(0, a.size, chunk):
         x = a[s:s + chunk].astype(np.float64)
@@ -58,10 +62,6 @@ def sumsq_diff(a, b, chunk=1 << 24):
 
 
 def rel(a, b):
-    a, b = np.asarray(a), np.asarray(b)
-    if a.flags.forc != b.flags.forc or (a.flags.f_contiguous != b.flags.f_contiguous):
-        a = np.asarray(a, order="F")
-        b = np.asarray(b, order="F")
     num, den = sumsq_diff(a, b)
     return float(np.sqrt(num) / (np.sqrt(den) if den > 0 else 1.0))
 
