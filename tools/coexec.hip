@@ -60,11 +60,11 @@ __device__ double work(int iters, double seed) {
         typedef float f4 __attribute__((ext_vector_type(4)));
         f4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
         float a = (float)seed, b = (float)seed * 0.5f;
-        for (int i = 0; i < iters * 2; ++i) {
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, c1, 0, 0, 0);
-            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, c2, 0, 0, 0);
-            c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, c3, 0, 0, 0);
+        for (int i = 0; i < iters * 2; ++i) {  // asm volatile: the builtin loop was folded away
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c0) : "v"(a), "v"(b));
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c1) : "v"(b), "v"(a));
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c2) : "v"(a), "v"(a));
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c3) : "v"(b), "v"(b));
         }
         out = c0[0] + c1[1] + c2[2] + c3[3];
     } else if (ROLE == 4) {

@@ -19,7 +19,7 @@ cp $O/${TAG}_c5_k5_traffic.json profiles/${TAG}_c5_k5_traffic.json
 # MFMA utilisation of K2 (k_m3_32) and K5: one SQ/GRBM pass, kernel counters only
 timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     --output-format csv -d $O/pmc_sq -o run -- $B > $O/pmc_sq.log 2>&1
-python3 tools/pmc_summary.py --json $O/${TAG}_c5_k2_mfma_util.json $O/pmc_sq "k_m3_32<256>" "k5_f32s<256>" > $O/${TAG}_c5_mfma_util.txt
+python3 tools/pmc_summary.py --json $O/${TAG}_c5_k2_mfma_util.json $O/pmc_sq "k_m3_32<256" "k5_f32s<256>" > $O/${TAG}_c5_mfma_util.txt
 cp $O/${TAG}_c5_k2_mfma_util.json profiles/${TAG}_c5_k2_mfma_util.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
     python3 bench.py --config 5 --no-cpu --no-e2e --steps 10 --warmup 3 > $O/stats.log 2>&1
