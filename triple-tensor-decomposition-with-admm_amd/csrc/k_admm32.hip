@@ -467,11 +467,17 @@ void k5_f32s(K5Args32 a) {
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
     auto gran = [](int c, int q) { return c * G + ((q + ((c * G) >> 4)) & (G - 1)); };
-    __shared__ __attribute__((aligned(16))) float sC[2][16 * LDC];
-    __shared__ float tsm[2][16 * 17];
+    // DEFER (LEAN 3): the h = 1 wave runs the W MFMAs of tile tt-1 during
+    // step tt (beside the chain of tt on its partner), from a T transpose
+    // buffer and a C^ slice one step old: no barrier between the chain and W,
+    // three C^ slices (tt-1 in use by h = 1, tt, tt+1 being staged) and two
+    // transpose buffers
+    constexpr bool DEFER = K5F_LEAN >= 3;
+    constexpr int NSL = DEFER ? 3 : 2;
+    __shared__ __attribute__((aligned(16))) float sC[NSL][16 * LDC];
+    __shared__ float tsm[2][DEFER ? 2 : 1][16 * 17];
     __shared__ float csm[2][128];
     __shared__ __attribute__((aligned(16))) f4 lx[2][2][64];  // [slot][half] partial L
-    float* ts = tsm[slot];
     float* cs = csm[slot];
     constexpr int WS = RP * 16 + 16;
     static_assert(2 * WS <= 2 * 16 * LDC, "k5_f32s: the W exchange reuses the C^ slices");
@@ -536,7 +542,21 @@ void k5_f32s(K5Args32 a) {
         // transpose buffer after one more barrier (its SIMD runs the other
         // resident wave meanwhile)
         constexpr bool CHAIN = !K5F_LEAN || h == 0;
-        auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+        // W^T += C^T T for this half's M-tiles (granules q in [h*GH, (h+1)*GH))
+        auto wmfma = [&](const float* cR, const float (&tr)[4]) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
+#pragma unroll
+                for (int q = 0; q < GH; ++q) {
+                    const f4 c = cW[gran(il, h * GH + q)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
+                }
+            }
+        };
+        auto body = [&](int64_t tt, int buf, int nbuf, Regs& cx, Regs& nx, bool pf) {
+            float* ts = tsm[slot][DEFER ? (int)(tt & 1) : 0];
             const int64_t tb = tbase(tt);
             const int64_t o = (tb >> 2) + lane;
             if (pf) {
@@ -607,24 +627,25 @@ void k5_f32s(K5Args32 a) {
                 for (int s = 0; s < 4; ++s) tv[s] = ts[il * 17 + 4 * s + tg];
                 T4[o] = tv;
             }
-            if (K5F_LEAN) {
-                __syncthreads();  // T of this tile in ts (h = 0 wrote it above)
-                if (h == 1)
+            if constexpr (DEFER && h == 1) {
+                // W of tile tt-1: its T (written by the partner in step tt-1,
+                // before that step's closing barrier) and its C^ slice
+                if (tt > 0) {
+                    const float* tp = tsm[slot][(int)((tt - 1) & 1)];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) tr[r] = ts[(4 * tg + r) * 17 + il];
-            }
-            // this half's W M-tiles: granules q in [h*GH, (h+1)*GH)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
-#pragma unroll
-                for (int q = 0; q < GH; ++q) {
-                    const f4 c = cW[gran(il, h * GH + q)];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
+                    for (int r = 0; r < 4; ++r) tr[r] = tp[(4 * tg + r) * 17 + il];
+                    wmfma(sC[(int)((tt + NSL - 1) % NSL)], tr);
                 }
+            } else {
+                if (K5F_LEAN && !DEFER) {
+                    __syncthreads();  // T of this tile in ts (h = 0 wrote it above)
+                    if (h == 1)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) tr[r] = ts[(4 * tg + r) * 17 + il];
+                }
+                wmfma(cR, tr);
             }
-            if (pf) stage_store(buf ^ 1);
+            if (pf) stage_store(nbuf);
             __syncthreads();
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -640,15 +661,40 @@ void k5_f32s(K5Args32 a) {
         stage_store(0);
         __syncthreads();
         int64_t tt = 0;
-        for (; tt + 2 < ntt; tt += 2) {
-            body(tt, 0, xa, xb, true);
-            body(tt + 1, 1, xb, xa, true);
-        }
-        if (tt + 1 < ntt) {
-            body(tt, 0, xa, xb, true);
-            body(tt + 1, 1, xb, xa, false);
+        if constexpr (DEFER) {
+            // slices rotate over three buffers: tile tt in tt % 3
+            int b0 = 0;
+            for (; tt + 2 < ntt; tt += 2) {
+                const int b1 = b0 == 2 ? 0 : b0 + 1, b2 = b1 == 2 ? 0 : b1 + 1;
+                body(tt, b0, b1, xa, xb, true);
+                body(tt + 1, b1, b2, xb, xa, true);
+                b0 = b2;
+            }
+            const int b1 = b0 == 2 ? 0 : b0 + 1, b2 = b1 == 2 ? 0 : b1 + 1;
+            if (tt + 1 < ntt) {
+                body(tt, b0, b1, xa, xb, true);
+                body(tt + 1, b1, b2, xb, xa, false);
+            } else {
+                body(tt, b0, b1, xa, xb, false);
+            }
+            if constexpr (h == 1) {  // the last tile's W (its T and slice are final: no staging after it)
+                float tr[4];
+                const float* tp = tsm[slot][(int)((ntt - 1) & 1)];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tr[r] = tp[(4 * tg + r) * 17 + il];
+                wmfma(sC[(int)((ntt - 1) % NSL)], tr);
+            }
         } else {
-            body(tt, 0, xa, xb, false);
+            for (; tt + 2 < ntt; tt += 2) {
+                body(tt, 0, 1, xa, xb, true);
+                body(tt + 1, 1, 0, xb, xa, true);
+            }
+            if (tt + 1 < ntt) {
+                body(tt, 0, 1, xa, xb, true);
+                body(tt + 1, 1, 0, xb, xa, false);
+            } else {
+                body(tt, 0, 1, xa, xb, false);
+            }
         }
         // W^T C/D layout: M-tile m row rho = 4(l>>4) + rr, col ij = l & 15,
         // k = rho * MT + m; this half's m = 4(h*GH + q) + u

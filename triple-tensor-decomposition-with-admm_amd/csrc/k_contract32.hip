@@ -180,9 +180,71 @@ __global__ __launch_bounds__(256) void k_m2_32v(const float* __restrict__ Wk,
     if (lane == 0) M2[j * RP + k] = (double)acc1;
 }
 
+// The same with the A^ row in registers: a wave owns one k and JB rows j, so
+// the row k of A^T (n1p doubles, rounded to single once) is loaded once per
+// JB rows instead of once per row (k_m2_32v re-read all of A^T for every j:
+// 8.6 GB of L2 traffic beside the 4.3 GB of W at config 5).  n1p <= 64*4*UG.
+template <int UG, int JB>
+__global__ __launch_bounds__(256) void k_m2_32w(const float* __restrict__ Wk,
+                                                const double* __restrict__ AhT, double* M2,
+                                                int64_t n1p, int64_t n2, int64_t plane, int RP,
+                                                const int* stop) {
+    if (*stop) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k = blockIdx.y;
+    const int64_t j0 = ((int64_t)blockIdx.x * 4 + w) * JB;
+    if (j0 >= n2) return;  // wave-uniform
+    const int64_t n4 = n1p >> 2;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2* ap = reinterpret_cast<const d2*>(AhT + (int64_t)k * n1p);
+    f4 a[UG];
+#pragma unroll
+    for (int u = 0; u < UG; ++u) {
+        const int64_t gi = lane + 64 * u;
+        if (gi < n4) {
+            const d2 x = ap[2 * gi], y = ap[2 * gi + 1];
+            a[u] = f4{(float)x[0], (float)x[1], (float)y[0], (float)y[1]};
+        } else {
+            a[u] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    }
+    const f4* wk = reinterpret_cast<const f4*>(Wk + (int64_t)k * plane);
+    for (int jj = 0; jj < JB; ++jj) {
+        const int64_t j = j0 + jj;
+        if (j >= n2) break;  // wave-uniform
+        const f4* wp = wk + j * n4;
+        f4 v[UG];
+#pragma unroll
+        for (int u = 0; u < UG; ++u) {
+            const int64_t gi = lane + 64 * u;
+            v[u] = gi < n4 ? __builtin_nontemporal_load(wp + gi) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+        f4 acc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < UG; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[u & 3][c] = fmaf(v[u][c], a[u][c], acc[u & 3][c]);
+        const f4 t4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        float s1 = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off);
+        if (lane == 0) M2[j * RP + k] = (double)s1;
+    }
+}
+
 void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
                   hipStream_t st) {
     const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;
+    const char* m2v = std::getenv("TRITD_M2V");  // A/B: 1 = k_m2_32v
+    constexpr int UG = 8, JB = 8;
+    if (!old && !(m2v && std::atoi(m2v) == 1) && g.n1p <= 64 * 4 * UG) {
+        hipLaunchKernelGGL((k_m2_32w<UG, JB>), dim3((unsigned)cdiv(g.n2, 4 * JB), (unsigned)g.RP),
+                           dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
     if (!old)
         hipLaunchKernelGGL(k_m2_32v, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
                            AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
