@@ -29,9 +29,11 @@
 #endif
 // k5_f32s: 0 both waves of a pair run the elementwise chain, 1 only one does,
 // 2 = 1 with the roles alternating between workgroups (round 5, interleaved
-// A/B at config 5: K5 15.73 -> 15.45 ms, iteration 23.72 -> 23.42 ms)
+// A/B at config 5: K5 15.73 -> 15.45 ms, iteration 23.72 -> 23.42 ms), 3 = 2
+// with the other wave's W MFMAs deferred by one t-tile (no barrier between
+// the chain and W: K5 15.49 -> 15.24 ms, iteration 22.23 -> 21.95 ms)
 #ifndef K5F_LEAN
-#define K5F_LEAN 2
+#define K5F_LEAN 3
 #endif
 
 namespace tritd {
