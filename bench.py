@@ -149,6 +149,9 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end one-shot calls")
+    ap.add_argument("--comm", default="rccl", choices=("rccl", "host"),
+                    help="N > 1: libtritd's RCCL communicator (default), or the host all-reduce "
+                         "transport over gloo (correctness rehearsal with ranks sharing a GPU)")
     # --algo als: triple_decomp_ALS.m on the config-4 workload
     ap.add_argument("--algo", default="admm", choices=("admm", "als"))
     args = ap.parse_args()
@@ -158,6 +161,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    host_comm = args.comm == "host"
     if world != args.gpus and world > 1:
         raise SystemExit("--gpus must match WORLD_SIZE")
 
@@ -165,8 +169,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        if host_comm:
+            # rehearsal of the N > 1 path on fewer GPUs than ranks: gloo for
+            # torch.distributed, libtritd's host all-reduce transport, ranks
+            # sharing devices round-robin (the timing is not a scaling number)
+            local_rank = local_rank % max(torch.cuda.device_count(), 1)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
 
     def barrier():
         if dist is not None:
@@ -194,9 +205,11 @@ def main():
     del data["D"], data["Lstar"]
 
     # mode-1 shard of this rank
-    from tritd.dist import make_comm, shard_bounds
+    from tritd.dist import make_comm, make_host_comm, shard_bounds
     i0, i1 = shard_bounds(n1, world, rank)
-    comm = make_comm(dist, rank, world, local_rank) if world > 1 else None
+    comm = None
+    if world > 1:
+        comm = (make_host_comm if host_comm else make_comm)(dist, rank, world, local_rank)
 
     # inputs resident in HBM before the timed region
     dev = torch.device("cuda", local_rank)
@@ -224,8 +237,10 @@ def main():
     probe_ms, probe_pick = sess.probe()
     dense1, _ = sess.counters()
     dense_per_launch = (dense1 - dense0) / K
+    # host-side collectives of the bench itself (gloo wants CPU tensors)
+    cdev = torch.device("cpu") if host_comm else dev
     if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if done != W + K or stopped:
@@ -248,7 +263,7 @@ def main():
     L_shard = torch.from_numpy(np.ascontiguousarray(Lstar[i0:i1].transpose(2, 1, 0))).to(dev)
     num, den = sess.rre_parts(L_shard.data_ptr(), i1 - i0)
     if dist is not None:
-        t = torch.tensor([num, den], device=dev, dtype=torch.float64)
+        t = torch.tensor([num, den], device=cdev, dtype=torch.float64)
         dist.all_reduce(t)
         num, den = float(t[0]), float(t[1])
     rre = float(np.sqrt(num / den))
@@ -331,7 +346,9 @@ def main():
                                    "(SURVEY.md 8d), traffic opts (traffic_triple_comparison.m:42-50)"
                                    % (args.config, n1, n2, n3, "fp32" if f32 else "fp64", r),
                        "n1": n1, "n2": n2, "n3": n3, "r": r, "maxIter": maxIter,
-                       "parallelism": "mode1-shard x%d" % world},
+                       "parallelism": "mode1-shard x%d" % world
+                                      + (" (host all-reduce rehearsal: not a scaling number)"
+                                         if host_comm and world > 1 else "")},
             "rre_final": rre,
             "k_final": k_final,
             "errHist_final": errhist_final,
