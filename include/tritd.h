@@ -105,7 +105,8 @@ tritd_status tritd_device_count(int32_t* count);
  *   A0,B0,C0: initial factors in reference layout (the MATLAB wrapper draws
  *             them with randn in the order of :23 so the RNG stream matches)
  *   A,B,C   : outputs, reference layout
- *   O, E    : outputs, n1*n2*n3 (E is the 6th, extra output; may be NULL)
+ *   O, E    : outputs, n1*n2*n3 (E is the 6th, extra output; either may be NULL, which also
+ *             skips its device-to-host transfer)
  *   errHist : capacity maxIter; *iters receives k (errHist = errHist(1:k), :68)
  * Runs on `device`; device = -1 runs on the device set of tritd_set_devices
  * (the current device when none is set).

@@ -153,22 +153,27 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mxArray* B = make3(r, n[1], r);
     mxArray* C = make3(r, r, n[2]);
     const mxClassID cls = single ? mxSINGLE_CLASS : mxDOUBLE_CLASS;
-    mxArray* O = make3(n[0], n[1], n[2], cls);
-    mxArray* E = make3(n[0], n[1], n[2], cls);
+    // O and E only when asked for: each is a full tensor to bring back over PCIe
+    // (the drivers take [A,B,C,O,errHist]; E is this build's 6th output)
+    mxArray* O = nlhs > 3 ? make3(n[0], n[1], n[2], cls) : nullptr;
+    mxArray* E = nlhs > 5 ? make3(n[0], n[1], n[2], cls) : nullptr;
     mxArray* eh = mxCreateDoubleMatrix(o.maxIter > 0 ? o.maxIter : 0, 1, mxREAL);
+    auto data = [](mxArray* x) { return x ? mxGetData(x) : nullptr; };
     int32_t k = 0;
     tritd_set_print_callback(print_line, nullptr);
     double* ehp = o.maxIter > 0 ? mxGetPr(eh) : nullptr;
     const tritd_status st =
         single ? tritd_admm_f32(static_cast<const float*>(mxGetData(D)), n[0], n[1], n[2], r, &o,
                                 mxGetPr(prhs[4]), mxGetPr(prhs[5]), mxGetPr(prhs[6]), mxGetPr(A),
-                                mxGetPr(B), mxGetPr(C), static_cast<float*>(mxGetData(O)),
-                                static_cast<float*>(mxGetData(E)), ehp, &k, -1)
+                                mxGetPr(B), mxGetPr(C), static_cast<float*>(data(O)),
+                                static_cast<float*>(data(E)), ehp, &k, -1)
                : tritd_admm_f64(mxGetPr(D), n[0], n[1], n[2], r, &o, mxGetPr(prhs[4]),
                                 mxGetPr(prhs[5]), mxGetPr(prhs[6]), mxGetPr(A), mxGetPr(B),
-                                mxGetPr(C), mxGetPr(O), mxGetPr(E), ehp, &k, -1);
+                                mxGetPr(C), static_cast<double*>(data(O)),
+                                static_cast<double*>(data(E)), ehp, &k, -1);
     if (st != TRITD_OK) {
-        for (mxArray* x : {A, B, C, O, E, eh}) mxDestroyArray(x);
+        for (mxArray* x : {A, B, C, O, E, eh})
+            if (x) mxDestroyArray(x);
         fail(st == TRITD_ERR_OPTS ? "MATLAB:nonExistentField" : "tritd:solver", status_msg(st));
     }
     warn_flags();
@@ -177,7 +182,7 @@ void do_admm(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     for (int q = 0; q < 6; ++q) {
         if (q < (nlhs > 0 ? nlhs : 1))
             plhs[q] = outs[q];
-        else
+        else if (outs[q])
             mxDestroyArray(outs[q]);
     }
 }

@@ -135,7 +135,8 @@ def triple_decomp_ADMM(D, r, opts, A0=None, B0=None, C0=None, *, device=-1, retu
     B = np.zeros((r, n2, r), order="F")
     Cf = np.zeros((r, r, n3), order="F")
     O = np.zeros((n1, n2, n3), order="F")
-    E = np.zeros((n1, n2, n3), order="F")
+    # E only when asked for (a full tensor more to bring back from the device)
+    E = np.zeros((n1, n2, n3), order="F") if return_E else None
     errHist = np.zeros(max(o.maxIter, 1))
     k = _lib.i32(0)
     if virtual_shards and virtual_shards > 1:
@@ -168,7 +169,7 @@ def _admm_f32(D, r, o, opts, A0, B0, C0, device, return_E, return_iters):
     B = np.zeros((r, n2, r), order="F")
     Cf = np.zeros((r, r, n3), order="F")
     O = np.zeros((n1, n2, n3), order="F", dtype=np.float32)
-    E = np.zeros((n1, n2, n3), order="F", dtype=np.float32)
+    E = np.zeros((n1, n2, n3), order="F", dtype=np.float32) if return_E else None
     errHist = np.zeros(max(o.maxIter, 1))
     k = _lib.i32(0)
     check_flags(lib.tritd_admm_f32(_ptr(D), n1, n2, n3, r, C.byref(o), _ptr(A0), _ptr(B0), _ptr(C0),
