@@ -74,9 +74,13 @@ AlsSession::AlsSession(int device, const double* X, int64_t ldX, int64_t n1, int
         } else {
             DBuf tmp;
             tmp.alloc((size_t)(g_.n1l * n2 * n3));
-            TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * sizeof(double), X, ldX * sizeof(double),
-                                       g_.n1l * sizeof(double), (size_t)(n2 * n3),
-                                       hipMemcpyHostToDevice, st_));
+            if (ldX == g_.n1l)  // contiguous: one 1-D copy (the 2-D form is slower from pageable memory)
+                TRITD_HIP(hipMemcpyAsync(tmp.p, X, (size_t)(g_.n1l * n2 * n3) * sizeof(double),
+                                         hipMemcpyHostToDevice, st_));
+            else
+                TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * sizeof(double), X, ldX * sizeof(double),
+                                           g_.n1l * sizeof(double), (size_t)(n2 * n3),
+                                           hipMemcpyHostToDevice, st_));
             launch_to_tm(g_, tmp.p, g_.n1l, X_.p, st_);
             TRITD_HIP(hipStreamSynchronize(st_));
         }
@@ -333,9 +337,13 @@ void AlsSession::get_O(double* O, int64_t ldO) {
         DBuf tmp;
         tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));
         launch_from_tm(g_, src, tmp.p, g_.n1l, st_);
-        TRITD_HIP(hipMemcpy2DAsync(O, ldO * sizeof(double), tmp.p, g_.n1l * sizeof(double),
-                                   g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
-                                   hipMemcpyDeviceToHost, st_));
+        if (ldO == g_.n1l)
+            TRITD_HIP(hipMemcpyAsync(O, tmp.p, (size_t)(g_.n1l * g_.n2 * g_.n3) * sizeof(double),
+                                     hipMemcpyDeviceToHost, st_));
+        else
+            TRITD_HIP(hipMemcpy2DAsync(O, ldO * sizeof(double), tmp.p, g_.n1l * sizeof(double),
+                                       g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
+                                       hipMemcpyDeviceToHost, st_));
         TRITD_HIP(hipStreamSynchronize(st_));
     }
 }
