@@ -526,19 +526,29 @@ void k5_f32s(K5Args32 a) {
     };
     double ssL = 0.0, ssO = 0.0;
     unsigned ndense = 0;
-    f4 wacc[MTH];
+    // SPLIT (LEAN 4): the pair splits by role instead of by rank: wave h = 0
+    // computes all of L (both K halves, summed in the same order as the
+    // exchange it replaces: results unchanged) and runs the chain; wave h = 1
+    // accumulates all of W, one t-tile late.  No L exchange, so one barrier
+    // per t-tile instead of two; 64 MFMAs per wave per t-tile either way.
+    constexpr bool SPLIT = K5F_LEAN >= 4;
+    static_assert(!SPLIT || DEFER, "k5_f32s: SPLIT builds on DEFER");
+    f4 wacc[SPLIT ? MT : MTH];
 
     // the walk, specialised per half (straight-line code in each)
     auto walk = [&](auto HC) {
         constexpr int h = decltype(HC)::value;
-        float kr[KSH];  // KR(ij = l & 15, k = (l>>4) * KS + h*KSH + s), single-rounded
+        constexpr int NKR = SPLIT ? (h == 0 ? KS : 0) : KSH;  // KR operands this wave holds
+        constexpr int NWT = SPLIT ? (h == 1 ? MT : 0) : MTH;  // W M-tiles this wave accumulates
+        // KR(ij = l & 15, k = (l>>4) * KS + k0 + s), single-rounded; k0 = h*KSH (rank split) or 0
+        float kr[NKR > 0 ? NKR : 1];
 #pragma unroll
-        for (int s = 0; s < KSH; ++s) {
-            const int k = tg * KS + h * KSH + s;
+        for (int s = 0; s < NKR; ++s) {
+            const int k = tg * KS + (SPLIT ? 0 : h * KSH) + s;
             kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
         }
 #pragma unroll
-        for (int m = 0; m < MTH; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int m = 0; m < NWT; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
         // LEAN: only the h = 0 wave of the pair loads the tile, decodes E and
         // runs the elementwise chain; the h = 1 wave takes T from the LDS
         // transpose buffer after one more barrier (its SIMD runs the other
@@ -546,12 +556,13 @@ void k5_f32s(K5Args32 a) {
         constexpr bool CHAIN = !K5F_LEAN || h == 0;
         // W^T += C^T T for this half's M-tiles (granules q in [h*GH, (h+1)*GH))
         auto wmfma = [&](const float* cR, const float (&tr)[4]) {
+            constexpr int NQ = NWT / 4, Q0 = SPLIT ? 0 : h * GH;  // granules of this wave
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
 #pragma unroll
-                for (int q = 0; q < GH; ++q) {
-                    const f4 c = cW[gran(il, h * GH + q)];
+                for (int q = 0; q < NQ; ++q) {
+                    const f4 c = cW[gran(il, Q0 + q)];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
                 }
@@ -576,20 +587,42 @@ void k5_f32s(K5Args32 a) {
                 if (pf) load_slot(tt + 2, cx.ce);
             }
             const float* cR = sC[buf];
-            f4 lacc[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
             const f4* cL = reinterpret_cast<const f4*>(cR + il * LDC);
+            f4 Lv = f4{0.0f, 0.0f, 0.0f, 0.0f};
+            if constexpr (SPLIT) {
+                if constexpr (h == 0) {  // both K halves, each summed as the exchange did
+                    f4 lp[2];
 #pragma unroll
-            for (int s4 = 0; s4 < KSH / 4; ++s4) {
-                const int gl = tg * (KS / 4) + h * (KSH / 4) + s4;
-                const f4 c = cL[gran(gl / G, gl % G)];
+                    for (int hh = 0; hh < 2; ++hh) {
+                        f4 lacc[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+                        for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                        for (int s4 = hh * (KSH / 4); s4 < (hh + 1) * (KSH / 4); ++s4) {
+                            const int gl = tg * (KS / 4) + s4;
+                            const f4 c = cL[gran(gl / G, gl % G)];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+                        }
+                        lp[hh] = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
+                    }
+                    Lv = lp[0] + lp[1];
+                }
+            } else {
+                f4 lacc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int s4 = 0; s4 < KSH / 4; ++s4) {
+                    const int gl = tg * (KS / 4) + h * (KSH / 4) + s4;
+                    const f4 c = cL[gran(gl / G, gl % G)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
+                }
+                lx[slot][h][lane] = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
+                __syncthreads();
+                Lv = lx[slot][0][lane] + lx[slot][1][lane];  // same order in both waves
             }
-            lx[slot][h][lane] = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
-            __syncthreads();
-            const f4 Lv = lx[slot][0][lane] + lx[slot][1][lane];  // same order in both waves
             float En[4], tr[4];
             f4 YLn, YOn;
 #pragma unroll
@@ -638,7 +671,7 @@ void k5_f32s(K5Args32 a) {
                     for (int r = 0; r < 4; ++r) tr[r] = tp[(4 * tg + r) * 17 + il];
                     wmfma(sC[(int)((tt + NSL - 1) % NSL)], tr);
                 }
-            } else {
+            } else if constexpr (!SPLIT) {
                 if (K5F_LEAN && !DEFER) {
                     __syncthreads();  // T of this tile in ts (h = 0 wrote it above)
                     if (h == 1)
@@ -703,10 +736,10 @@ void k5_f32s(K5Args32 a) {
         float* wl = &sC[0][0];  // the C^ slices are dead after the walk
         __syncthreads();
 #pragma unroll
-        for (int mq = 0; mq < MTH; ++mq)
+        for (int mq = 0; mq < NWT; ++mq)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int m = 4 * h * GH + mq;
+                const int m = (SPLIT ? 0 : 4 * h * GH) + mq;
                 const int k = (4 * tg + rr) * MT + m;
                 wl[slot * WS + k * 16 + il] = wacc[mq][rr];
             }
