@@ -337,10 +337,11 @@ void AlsSession::get_O(double* O, int64_t ldO) {
         DBuf tmp;
         tmp.alloc((size_t)(g_.n1l * g_.n2 * g_.n3));
         launch_from_tm(g_, src, tmp.p, g_.n1l, st_);
-        if (ldO == g_.n1l)
-            TRITD_HIP(hipMemcpyAsync(O, tmp.p, (size_t)(g_.n1l * g_.n2 * g_.n3) * sizeof(double),
-                                     hipMemcpyDeviceToHost, st_));
-        else
+        if (ldO == g_.n1l) {
+            const size_t nb = (size_t)(g_.n1l * g_.n2 * g_.n3) * sizeof(double);
+            populate_output(O, nb);
+            TRITD_HIP(hipMemcpyAsync(O, tmp.p, nb, hipMemcpyDeviceToHost, st_));
+        } else
             TRITD_HIP(hipMemcpy2DAsync(O, ldO * sizeof(double), tmp.p, g_.n1l * sizeof(double),
                                        g_.n1l * sizeof(double), (size_t)(g_.n2 * g_.n3),
                                        hipMemcpyDeviceToHost, st_));

@@ -867,6 +867,7 @@ tritd_status tritd_triple_product_qi_f64(const double* A, const double* B, const
         const tritd_status s =
             tritd_dev_triple_product_qi_f64(dA.p, dB.p, dC.p, n1, n2, n3, r, dX.p, nullptr);
         if (s != TRITD_OK) throw Error(s, g_last_error);
+        populate_output(X, dX.n * 8);
         TRITD_HIP(hipMemcpy(X, dX.p, dX.n * 8, hipMemcpyDeviceToHost));
     });
 }
@@ -885,6 +886,7 @@ tritd_status tritd_triple_product_f64(const double* A, const double* B, const do
         TRITD_HIP(hipMemcpy(dC.p, C, dC.n * 8, hipMemcpyHostToDevice));
         const tritd_status s = tritd_dev_triple_product_f64(dA.p, dB.p, dC.p, n1, n2, n3, r, dX.p, nullptr);
         if (s != TRITD_OK) throw Error(s, g_last_error);
+        populate_output(X, dX.n * 8);
         TRITD_HIP(hipMemcpy(X, dX.p, dX.n * 8, hipMemcpyDeviceToHost));
     });
 }
@@ -918,6 +920,7 @@ tritd_status tritd_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n
         TRITD_HIP(hipMemcpy(a.p, X, n * 8, hipMemcpyHostToDevice));
         const tritd_status s = tritd_dev_unfold_f64(a.p, n1, n2, n3, mode, b.p, nullptr);
         if (s != TRITD_OK) throw Error(s, g_last_error);
+        populate_output(Xn, n * 8);
         TRITD_HIP(hipMemcpy(Xn, b.p, n * 8, hipMemcpyDeviceToHost));
     });
 }
@@ -942,6 +945,7 @@ tritd_status tritd_soft_threshold_f64(const double* X, int64_t n, double lam, do
         a.alloc(n); b.alloc(n);
         TRITD_HIP(hipMemcpy(a.p, X, n * 8, hipMemcpyHostToDevice));
         launch_soft_threshold(a.p, n, lam, b.p, nullptr);
+        populate_output(Y, n * 8);
         TRITD_HIP(hipMemcpy(Y, b.p, n * 8, hipMemcpyDeviceToHost));
     });
 }
@@ -960,6 +964,7 @@ tritd_status tritd_build_design_f64(char which, const double* P, const double* Q
         TRITD_HIP(hipMemcpy(dP.p, P, dP.n * 8, hipMemcpyHostToDevice));
         TRITD_HIP(hipMemcpy(dQ.p, Q, dQ.n * 8, hipMemcpyHostToDevice));
         launch_design(which, dP.p, dQ.p, nP, nQ, r, dO.p, nullptr);
+        populate_output(out, dO.n * 8);
         TRITD_HIP(hipMemcpy(out, dO.p, dO.n * 8, hipMemcpyDeviceToHost));
     });
 }

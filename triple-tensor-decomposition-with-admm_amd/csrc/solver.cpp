@@ -11,10 +11,13 @@
 // several sessions on one device instead.
 #include "solver.h"
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace tritd {
 
@@ -474,6 +477,26 @@ void Session::launch_k5_any(int k, bool prologue) {
         k5side_ = SideSolve{};
     }
     launch_k5(g_, a, prologue, dy_, st_);
+}
+
+void populate_output(void* p, size_t bytes) {
+    if (!p || bytes < ((size_t)64 << 20)) return;
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23  // Linux 5.14
+#endif
+    constexpr uintptr_t PG = 4096, GR = (uintptr_t)2 << 20;
+    const uintptr_t a = ((uintptr_t)p + PG - 1) & ~(PG - 1);
+    const uintptr_t e = ((uintptr_t)p + bytes) & ~(PG - 1);
+    if (e <= a) return;
+    const unsigned hc = std::thread::hardware_concurrency();
+    const uintptr_t nt = std::min<uintptr_t>(16, hc ? hc : 1);
+    const uintptr_t chunk = (((e - a) / nt) + GR - 1) & ~(GR - 1);
+    std::vector<std::thread> th;
+    for (uintptr_t s = a; s < e; s += chunk) {
+        const size_t len = (size_t)std::min(chunk, e - s);
+        th.emplace_back([s, len] { (void)madvise((void*)s, len, MADV_POPULATE_WRITE); });
+    }
+    for (auto& t : th) t.join();
 }
 
 void comm_allreduce(tritd_comm* c, double* buf, int64_t count, bool max, hipStream_t st) {
@@ -1018,11 +1041,11 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
                 launch_from_tm32(g_, reinterpret_cast<float*>(pr.second), tmp.f(), g_.n1l, st_);
             else
                 launch_from_tm(g_, pr.second, tmp.p, g_.n1l, st_);
-            if (ldOE == g_.n1l)  // a whole tensor (one-shot calls): one contiguous copy; the
-                                 // 2-D form into pageable memory ran at ~15 GB/s, 1-D at ~55
-                TRITD_HIP(hipMemcpyAsync(pr.first, tmp.p, (size_t)(g_.n1l * g_.n2 * g_.n3) * es_,
-                                         hipMemcpyDeviceToHost, st_));
-            else
+            if (ldOE == g_.n1l) {  // a whole tensor (one-shot calls): one contiguous copy
+                const size_t nb = (size_t)(g_.n1l * g_.n2 * g_.n3) * es_;
+                populate_output(pr.first, nb);
+                TRITD_HIP(hipMemcpyAsync(pr.first, tmp.p, nb, hipMemcpyDeviceToHost, st_));
+            } else
                 TRITD_HIP(hipMemcpy2DAsync(pr.first, ldOE * es_, tmp.p, g_.n1l * es_, g_.n1l * es_,
                                            (size_t)(g_.n2 * g_.n3), hipMemcpyDeviceToHost, st_));
             TRITD_HIP(hipStreamSynchronize(st_));

@@ -17,6 +17,13 @@ struct tritd_comm {
 
 namespace tritd {
 
+// Host output buffers of a device-to-host copy: populate their pages in
+// parallel first (MADV_POPULATE_WRITE on up to 16 threads; content unchanged).
+// A fresh array (numpy zeros, mxCreate*) is mapped lazily, and the copy into
+// it then runs at the single-threaded page-fault rate (~16 GB/s measured
+// against ~55 GB/s into populated memory).  No-op below 64 MB.
+void populate_output(void* p, size_t bytes);
+
 // In-place all-reduce (sum, or max) of `count` doubles over the comm's ranks,
 // ordered on stream st: ncclAllReduce, or the host transport (drains st).
 void comm_allreduce(tritd_comm* c, double* buf, int64_t count, bool max, hipStream_t st);
