@@ -53,3 +53,24 @@ for rep in range(2):
     x = np.empty(N)
     ms, _ = t(lambda: np.copyto(x, h_pin.numpy()))
     print("host memcpy 1 thread %.1f ms = %.1f GB/s" % (ms, N * 8 / ms / 1e6), flush=True)
+# host page population on this box (Python threads + libc madvise): the cost the
+# library's populate_output pays before a 1 GB device-to-host copy
+import ctypes
+import threading
+libc = ctypes.CDLL("libc.so.6", use_errno=True)
+libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+for huge in (False, True):
+    for nt in (1, 16):
+        a = np.zeros(N)
+        p = a.ctypes.data
+        s0 = (p + 4095) & ~4095
+        e = (p + a.nbytes) & ~4095
+        t0 = time.perf_counter()
+        if huge:
+            h0 = (p + (2 << 20) - 1) & ~((2 << 20) - 1)
+            libc.madvise(h0, (e - h0) & ~((2 << 20) - 1), 14)
+        ch = ((e - s0) // nt + (2 << 20) - 1) & ~((2 << 20) - 1)
+        ths = [threading.Thread(target=lambda s=s: libc.madvise(s, min(ch, e - s), 23)) for s in range(s0, e, ch)]
+        [t_.start() for t_ in ths]
+        [t_.join() for t_ in ths]
+        print("populate 1 GB: huge %s, %d threads: %.1f ms" % (huge, nt, (time.perf_counter() - t0) * 1e3))

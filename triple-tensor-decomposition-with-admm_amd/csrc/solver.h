@@ -18,7 +18,8 @@ struct tritd_comm {
 namespace tritd {
 
 // Host output buffers of a device-to-host copy: populate their pages in
-// parallel first (MADV_POPULATE_WRITE on up to 16 threads; content unchanged).
+// parallel first (MADV_HUGEPAGE, then MADV_POPULATE_WRITE on up to 16
+// threads; content unchanged).
 // A fresh array (numpy zeros, mxCreate*) is mapped lazily, and the copy into
 // it then runs at the single-threaded page-fault rate (~16 GB/s measured
 // against ~55 GB/s into populated memory).  No-op below 64 MB.
