@@ -180,19 +180,23 @@ int mock_admm(const void* D, long n1, long n2, long n3, int r, const char* opt_n
     int rc = 0;
     g_printed.clear();
     try {
-        mexFunction(6, out, (int)in.size(), const_cast<const mxArray**>(in.data()));
+        // E == NULL: the drivers' five-output call [A,B,C,O,errHist] (nargout 5)
+        const int nlhs = E ? 6 : 5;
+        mexFunction(nlhs, out, (int)in.size(), const_cast<const mxArray**>(in.data()));
+        if (nlhs == 5 && out[5]) throw MockMexError{"mock:nlhs", "a 6th output for nargout 5"};
         const size_t nA = (size_t)n1 * r * r, nB = (size_t)r * n2 * r, nC = (size_t)r * r * n3;
         const size_t N = (size_t)n1 * n2 * n3;
         std::memcpy(A, out[0]->data.data(), nA * 8);
         std::memcpy(B, out[1]->data.data(), nB * 8);
         std::memcpy(C, out[2]->data.data(), nC * 8);
         const size_t es = single ? 4 : 8;
-        if ((out[3]->cls == mxSINGLE_CLASS) != (single != 0) || (out[5]->cls == mxSINGLE_CLASS) != (single != 0))
+        if ((out[3]->cls == mxSINGLE_CLASS) != (single != 0) ||
+            (E && (out[5]->cls == mxSINGLE_CLASS) != (single != 0)))
             throw MockMexError{"mock:class", "O/E class differs from the class of D"};
         std::memcpy(O, mxGetData(out[3]), N * es);
         *k = (int)out[4]->dims[0];
         std::memcpy(errHist, out[4]->data.data(), (size_t)*k * 8);
-        std::memcpy(E, mxGetData(out[5]), N * es);
+        if (E) std::memcpy(E, mxGetData(out[5]), N * es);
     } catch (const MockMexError& e) {
         std::snprintf(err, errlen, "%s|%s", e.id.c_str(), e.msg.c_str());
         rc = 1;

@@ -28,7 +28,7 @@ def gw(tmp_path_factory):
     return lib
 
 
-def run(gw, g, names=None, vals=None, single=False):
+def run(gw, g, names=None, vals=None, single=False, want_E=True):
     D = np.asfortranarray(g["D"], dtype=np.float32 if single else np.float64)
     n1, n2, n3 = D.shape
     r = g["r"]
@@ -47,8 +47,8 @@ def run(gw, g, names=None, vals=None, single=False):
     p = lambda a: C.c_void_p(a.ctypes.data)
     A0, B0, C0 = (np.asfortranarray(g[x]) for x in ("A0", "B0", "C0"))
     rc = gw.mock_admm(p(D), n1, n2, n3, r, ",".join(names).encode(), p(vals), p(A0), p(B0), p(C0),
-                      p(A), p(B), p(Cc), p(O), p(E), p(eh), C.byref(k), err, 1024, pr, 4096,
-                      int(single))
+                      p(A), p(B), p(Cc), p(O), p(E) if want_E else None, p(eh), C.byref(k), err,
+                      1024, pr, 4096, int(single))
     return rc, err.value.decode(), dict(A=A, B=B, C=Cc, O=O, E=E, errHist=eh[: k.value], k=k.value,
                                         printed=pr.value.decode())
 
@@ -80,6 +80,17 @@ def test_gateway_solve_matches_golden(gw, name):
     assert rel(orc.triple_product(res["A"], res["B"], res["C"]),
                orc.triple_product(g["A"], g["B"], g["C"])) <= 1e-9
     assert rel(res["O"], g["O"]) <= 1e-9 and rel(res["E"], g["E"]) <= 1e-9
+    np.testing.assert_allclose(res["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
+
+
+@pytest.mark.gpu
+def test_gateway_five_outputs_skip_E(gw):
+    """[A,B,C,O,errHist] = triple_decomp_ADMM(...) (nargout 5, the drivers' call):
+    no 6th output is created, the five match the golden."""
+    g = load_golden("g30_r3")
+    rc, err, res = run(gw, g, want_E=False)
+    assert rc == 0, err
+    assert res["k"] == g["k"] and rel(res["O"], g["O"]) <= 1e-9
     np.testing.assert_allclose(res["errHist"], g["errHist"], rtol=1e-8, atol=1e-13)
 
 
