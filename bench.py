@@ -174,10 +174,11 @@ def main():
             # torch.distributed, libtritd's host all-reduce transport, ranks
             # sharing devices round-robin (the timing is not a scaling number)
             local_rank = local_rank % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local_rank)
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
+            torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", rank=rank, world_size=world)
-        torch.cuda.set_device(local_rank)
 
     def barrier():
         if dist is not None:
