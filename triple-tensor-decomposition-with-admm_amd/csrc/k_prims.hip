@@ -4,6 +4,8 @@
 //   K6 soft_threshold  soft_threshold.m:2  (16 B/lane streaming)
 //   triple_product     triple_product.m:6  (MFMA, same tile as K5's L)
 //   buildF/G/H         buildF.m:17-21 etc. (design matrices, for parity only)
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace tritd {
@@ -355,7 +357,7 @@ __device__ __forceinline__ double st1(double x, double lam) {
 // for one load per grid-stride step).  Round 5 (tools/st_probe.hip, one box):
 // four loads per thread 0.332 ms = 6.46 TB/s, eight 0.337, sixteen 0.358; an
 // XCD-major or 1 MB-strided block order 0.36-0.37.
-constexpr int ST_U = 4;
+template <int ST_U>
 __global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict__ X, int64_t n,
                                                         double lam, double* __restrict__ Y) {
     const int64_t n2 = n >> 1;
@@ -383,10 +385,15 @@ __global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict
 
 void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hipStream_t st) {
     if (((uintptr_t)X | (uintptr_t)Y) & 15) throw Error(TRITD_ERR_ARG, "soft_threshold: 16-B alignment");
-    int64_t blocks = cdiv(n / 2, 256 * ST_U);
+    const char* ue = std::getenv("TRITD_ST_U");  // A/B (read per launch)
+    const int u = ue ? std::atoi(ue) : 8;
+    int64_t blocks = cdiv(n / 2, 256 * (u == 4 ? 4 : 8));
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_soft_threshold, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
+    if (u == 4)
+        hipLaunchKernelGGL(k_soft_threshold<4>, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
+    else
+        hipLaunchKernelGGL(k_soft_threshold<8>, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
     TRITD_CHECK_LAUNCH();
 }
 
