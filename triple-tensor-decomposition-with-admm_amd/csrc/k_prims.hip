@@ -354,9 +354,11 @@ __device__ __forceinline__ double st1(double x, double lam) {
 // ST_U 16-B nontemporal loads per thread issued before the first store, a
 // block owning ST_U * 256 consecutive pairs per step (tools/prim_stream.hip at
 // 512^3: 0.339 ms = 6.33 TB/s, the plain-copy ceiling of the chip, vs 0.39-0.41 ms
-// for one load per grid-stride step).  Round 5 (tools/st_probe.hip, one box):
-// four loads per thread 0.332 ms = 6.46 TB/s, eight 0.337, sixteen 0.358; an
-// XCD-major or 1 MB-strided block order 0.36-0.37.
+// for one load per grid-stride step).  Round 5: on zeros four loads per thread
+// timed 0.332 vs 0.337 ms (tools/st_probe.hip; sixteen 0.358, an XCD-major or
+// 1 MB-strided block order 0.36-0.37), but on random data, interleaved in one
+// process (tools/ab_st.py), eight win: 0.3415 vs 0.3459 ms = 6.29 TB/s, the
+// copy ceiling.  TRITD_ST_U=4 keeps the other for A/B.
 template <int ST_U>
 __global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict__ X, int64_t n,
                                                         double lam, double* __restrict__ Y) {
