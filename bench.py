@@ -30,7 +30,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA, dense
 F64_MFMA_PEAK_TFS = 78.6  # MI355X_MICROARCH.md: f64 MFMA, dense
 # SURVEY.md §8d workloads: (n1, n2, n3, r, dtype)
-CONFIGS = {4: (512, 512, 512, 8, "f64"), 5: (2048, 2048, 256, 16, "f32")}
+# (configs 2 and 3 are the reference's real-data experiments, run on
+# synthetic stand-ins of their shapes: tritd.synth.sensor_like / video_like)
+CONFIGS = {2: (54, 4, 1152, 5, "f64"), 3: (240, 320, 300, 5, "f64"),
+           4: (512, 512, 512, 8, "f64"), 5: (2048, 2048, 256, 16, "f32")}
+WORKLOADS = {
+    2: "config 2: sensor-shaped stand-in 54x4x1152 r=5 fp64, 10%% entries zeroed, traffic opts "
+       "(traffic_triple_comparison.m:27-50)",
+    3: "config 3: Highway-shaped stand-in 240x320x300 r=5 fp64 video, video opts "
+       "(video_triple_comparison.m:41-54)",
+    4: "config 4: synthetic 512x512x512 fp64 r=8 low-rank + 5%% outliers (SURVEY.md 8d), traffic "
+       "opts (traffic_triple_comparison.m:42-50)",
+    5: "config 5: synthetic 2048x2048x256 fp32 r=16 low-rank + 5%% outliers (SURVEY.md 8d), "
+       "traffic opts (traffic_triple_comparison.m:42-50)",
+}
 
 
 def ensure_built():
@@ -199,9 +212,16 @@ def main():
     cpu_iters = args.cpu_iters if args.cpu_iters is not None else (1 if f32 else 40)
     K, W = args.steps, args.warmup
     maxIter = max(100, K + W)
-    opts = dict(synth.TRAFFIC_OPTS, maxIter=maxIter, tol=synth.TRAFFIC_OPTS["tol"])
-    # config 5 uses the same recipe, rounded to single
-    data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    base_opts = synth.VIDEO_OPTS if args.config == 3 else synth.TRAFFIC_OPTS
+    opts = dict(base_opts, maxIter=maxIter, tol=base_opts["tol"])
+    if args.config == 2:  # RRE against the complete readings (traffic_triple_comparison.m:62)
+        data = synth.sensor_like(n1, n2, n3, r, missing=0.10, seed=0, init_seed=123)
+        data["Lstar"] = data.pop("X")
+    elif args.config == 3:  # RRE of the low-rank part against the frames
+        data = synth.video_like(n1, n2, n3, r, seed=0, init_seed=123)
+        data["Lstar"] = data.pop("X")
+    else:  # config 5 uses the same recipe, rounded to single
+        data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
     D, Lstar = data["D"].astype(npdt, order="F"), data["Lstar"].astype(npdt, order="F")
     del data["D"], data["Lstar"]
 
@@ -291,7 +311,9 @@ def main():
     gbs = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
     tfs = k5_flops / (k5_ms * 1e-3) / 1e12 if k5_ms > 0 else None
     # the committed PMC pass is of the 1-GPU launch (a shard moves 1/N of it)
-    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
+    # (committed PMC passes exist for configs 4 and 5 at their default shapes)
+    pmc_ok = world == 1 and args.config in (4, 5) and args.n is None and args.r is None
+    traffic, traffic_src = pmc_traffic(args.config) if pmc_ok else (None, None)
     if f32:  # config 5 is MFMA-bound
         roof = {"bound": "mfma", "achieved": tfs, "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": (tfs / F32_MFMA_PEAK_TFS) if tfs else None,
@@ -313,7 +335,7 @@ def main():
     k2_flops = 2.0 * N_local * r * r
     k2_tfs = k2_flops / (k2_ms * 1e-3) / 1e12 if k2_ms > 0 else None
     k2_peak = F32_MFMA_PEAK_TFS if f32 else F64_MFMA_PEAK_TFS
-    pmc_util, pmc_src = pmc_mfma_util(args.config) if world == 1 else (None, None)
+    pmc_util, pmc_src = pmc_mfma_util(args.config) if pmc_ok else (None, None)
     roof["mfma_gemm"] = {"kernel": "k_m3_cp (mode-3 MTTKRP, X3*H' of triple_decomp_ADMM.m:93)",
                          "achieved": k2_tfs, "peak": k2_peak, "unit": "TFLOP/s",
                          "frac": (k2_tfs / k2_peak) if k2_tfs else None,
@@ -343,9 +365,9 @@ def main():
             "vs_baseline": None,
             "dtype": dts,
             "data": "synthetic",
-            "config": {"workload": "config %d: synthetic %dx%dx%d %s r=%d low-rank + 5%% outliers "
-                                   "(SURVEY.md 8d), traffic opts (traffic_triple_comparison.m:42-50)"
-                                   % (args.config, n1, n2, n3, "fp32" if f32 else "fp64", r),
+            "config": {"workload": (WORKLOADS[args.config] if args.n is None and args.r is None
+                                    else "config %d shape override: %dx%dx%d r=%d"
+                                    % (args.config, n1, n2, n3, r)).replace("%%", "%"),
                        "n1": n1, "n2": n2, "n3": n3, "r": r, "maxIter": maxIter,
                        "parallelism": "mode1-shard x%d" % world
                                       + (" (host all-reduce rehearsal: not a scaling number)"
