@@ -303,8 +303,10 @@ def main():
     N_local = nl * n2 * n3
     tile_b = 256 * s_b
     streams, slots = sess.k5_profile()
+    # (dense-E mode, sess.k5_profile() = (7, 0): every E access is a dense stream)
     k5_bytes = int(streams * N_local * s_b + slots * tiles_per_launch * 256
-                   + (slots - 1) * dense_per_launch * tile_b + r * r * nl * n2 * s_b)
+                   + (max(slots - 1, 0) * dense_per_launch * tile_b if slots else 0)
+                   + r * r * nl * n2 * s_b)
     # flops: L(ij,t) = sum_k (Ah*Bh)(ij,k) Ch(t,k) and W = T x3 Ch, 2 N R each
     k5_flops = 4.0 * N_local * r * r
     k5_ms = km["fused_update"]

@@ -289,9 +289,15 @@ __device__ __forceinline__ void ce_encode_r(const double (&En)[4], int lane, dou
 
 // Two waves per SIMD (VGPRs + AGPRs <= 256): at one wave per SIMD the
 // streams do not keep enough bytes in flight (measured +6 % K5 time).
-template <int RP, bool PRO, bool DY>
+// DE (dense-E mode, DY only): E^(k), E^(k-1) and E^(k+1) live densely in the
+// tile-major E buffers for every tile — no compact slots are read, decoded,
+// encoded or written.  The session switches to it once E has turned dense
+// (video-like data: every tile overflows its slot and the compact form only
+// adds the slot traffic and the decode/encode work; solver.cpp run()).
+template <int RP, bool PRO, bool DY, bool DE = false>
 __global__ __launch_bounds__(64 * K5_WAVES) __attribute__((amdgpu_waves_per_eu(RP >= 128 ? 1 : K5_WPE, K5_WPE)))
 void k5_fused(K5Args a) {
+    static_assert(!DE || (DY && !PRO), "k5_fused: dense-E mode is a derived-Y_O update");
     if (*a.stop) return;
     // side job: workgroup 0 runs the R x R solve of the next update_A
     // (sweep.h) beside the walk, so no second stream is needed for it
@@ -518,6 +524,7 @@ void k5_fused(K5Args a) {
     const int vslot = (lane & 31) * 8;
 #endif
     auto load_slot = [&](int64_t tt, Regs& rx) {
+        if constexpr (DE) return;
         const int64_t t2 = tt < ntt ? tt : ntt - 1;  // clamped: no branch
 #if K5_BUF
         if (!PRO) {
@@ -574,6 +581,10 @@ void k5_fused(K5Args a) {
 #endif
             stage_load(PIPE ? (tt + 2 < ntt ? tt + 2 : ntt - 1) : tt + 1);
             load(tt + 1, nx);
+            if constexpr (DE) {  // both E tiles are part of the regular batch
+                load_dense(tt + 1, nx);
+                load_dense_p(tt + 1, nx);
+            }
             // keep the prefetch ahead of the compute: the scheduler otherwise
             // sinks it next to the stores (less register pressure, no latency
             // hiding)
@@ -581,12 +592,20 @@ void k5_fused(K5Args a) {
             // rare, wave-uniform: tile tt+1 overflowed last time.  Issued after
             // the batch and consumed a step later, so the common path's waits
             // stay exact
-            if (!PRO && dn1) load_dense(tt + 1, nx);
-            if (!PRO && DY && dnp1) load_dense_p(tt + 1, nx);
+            if (!DE && !PRO && dn1) load_dense(tt + 1, nx);
+            if (!DE && !PRO && DY && dnp1) load_dense_p(tt + 1, nx);
         }
         K5_PT(1);
         double ev[4], evp[4];
-        if (!PRO) {
+        if constexpr (DE) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    ev[2 * p + q] = cx.ed[p][q];
+                    evp[2 * p + q] = cx.edp[p][q];
+                }
+        } else if (!PRO) {
 #if K5_SMASK
             const int64_t sc0 = (tb >> 8) * CE_SLOT;
             uint64_t mk[4];
@@ -769,11 +788,17 @@ void k5_fused(K5Args a) {
                 if (!DY) st2(YOn2, YO2 + o + 64 * p);
             }
             K5_PT(4);
+            if constexpr (DE) {  // E^(k+1) over E^(k-1), densely
+                st2(d2v{En[0], En[1]}, Eout2 + o);
+                st2(d2v{En[2], En[3]}, Eout2 + o + 64);
+                ++ndense;
+            } else {
 #if K5_BUF
-            ce_encode_r(En, lane, cs, DY ? rCEp : rCE, (int)(phys(tt) * 1024), Eout2, o, ndense);
+                ce_encode_r(En, lane, cs, DY ? rCEp : rCE, (int)(phys(tt) * 1024), Eout2, o, ndense);
 #else
-            ce_encode(En, lane, cs, CEout, (tb >> 8) * CE_SLOT, Eout2, o, ndense);
+                ce_encode(En, lane, cs, CEout, (tb >> 8) * CE_SLOT, Eout2, o, ndense);
 #endif
+            }
             K5_PT(5);
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
@@ -842,8 +867,8 @@ void k5_fused(K5Args a) {
         load_slot(1, xb);
     }
     load(0, xa);
-    if (!PRO && ce_is_dense(xa.ce)) load_dense(0, xa);
-    if (!PRO && DY && ce_is_dense(xa.cep)) load_dense_p(0, xa);
+    if (DE || (!PRO && ce_is_dense(xa.ce))) load_dense(0, xa);
+    if (DE || (!PRO && DY && ce_is_dense(xa.cep))) load_dense_p(0, xa);
     stage(0, 0);
     if (PIPE) stage(ntt > 1 ? 1 : 0, 1);
     __syncthreads();
@@ -923,17 +948,21 @@ extern "C" int tritd_k5prof(unsigned long long* out) {
 namespace tritd {
 #endif
 
-void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st) {
+void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st, bool dense_e) {
     if (a.side.on && (prologue || g.RP > 64)) throw Error(TRITD_ERR_ARG, "K5 side solve: RP <= 64 only");
+    if (dense_e && (prologue || !dy || g.RP > 64))
+        throw Error(TRITD_ERR_ARG, "K5 dense-E mode: derived-Y_O update, RP <= 64");
     const dim3 grid(k5_grid(g) + (a.side.on ? 1 : 0)), block(64 * K5_WAVES);
-#define K5_CASE(RPV)                                                                 \
-    case RPV:                                                                        \
-        if (prologue)                                                                \
-            hipLaunchKernelGGL((k5_fused<RPV, true, false>), grid, block, 0, st, a); \
-        else if (dy)                                                                 \
-            hipLaunchKernelGGL((k5_fused<RPV, false, true>), grid, block, 0, st, a); \
-        else                                                                         \
-            hipLaunchKernelGGL((k5_fused<RPV, false, false>), grid, block, 0, st, a); \
+#define K5_CASE(RPV)                                                                       \
+    case RPV:                                                                              \
+        if (prologue)                                                                      \
+            hipLaunchKernelGGL((k5_fused<RPV, true, false>), grid, block, 0, st, a);       \
+        else if (dy && dense_e && RPV <= 64)                                               \
+            hipLaunchKernelGGL((k5_fused<RPV, false, true, (RPV <= 64)>), grid, block, 0, st, a); \
+        else if (dy)                                                                       \
+            hipLaunchKernelGGL((k5_fused<RPV, false, true>), grid, block, 0, st, a);       \
+        else                                                                               \
+            hipLaunchKernelGGL((k5_fused<RPV, false, false>), grid, block, 0, st, a);      \
         break;
     switch (g.RP) {
         K5_CASE(16)

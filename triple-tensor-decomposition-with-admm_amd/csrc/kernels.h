@@ -59,7 +59,9 @@ struct K5Args {
 };
 int k5_grid(const Geom& g);
 int k5_parts32(const Geom& g);  // fp32 K5's norm-partial count (its workgroups)
-void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st);
+// dense_e: E kept densely for every tile (no compact slots; dy only, RP <= 64)
+void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st,
+               bool dense_e = false);
 // O_k = (D + invL_next*Y_L) - T_{k+1} (O is not stored by K5)
 void launch_pool_probe(const Geom& g, double* D, double* YL, double* YO, double* T, double* CE,
                        bool dy, hipStream_t st);

@@ -105,6 +105,8 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         sb_main_ = !(sbm && std::atoi(sbm) == 0);
         const char* gms = std::getenv("TRITD_GRAM_MAIN_SH");  // sharded schedule
         gram_main_sh_ = gms ? std::atoi(gms) : 0;
+        const char* de = std::getenv("TRITD_DENSE_E");
+        de_mode_ = de ? std::atoi(de) : -1;
         const char* sh = std::getenv("TRITD_SHOV");
         shov_ = comm != nullptr && comm->active() && shared_stream == nullptr &&
                 !(sh && std::atoi(sh) == 0);
@@ -115,6 +117,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
             TRITD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     qi_ = o_.model == TRITD_MODEL_QI;
+    de_ = de_mode_ == 1 && de_eligible();  // forced from the start (E starts at zero)
     if (o_.model != TRITD_MODEL_CP && o_.model != TRITD_MODEL_QI)
         throw Error(TRITD_ERR_ARG, "opts.model must be 'cp' or 'qi'");
     if (qi_ && f32_)
@@ -476,7 +479,28 @@ void Session::launch_k5_any(int k, bool prologue) {
         a.side = k5side_;
         k5side_ = SideSolve{};
     }
-    launch_k5(g_, a, prologue, dy_, st_);
+    launch_k5(g_, a, prologue, dy_, st_, de_ && !prologue);
+}
+
+// Dense-E mode switch (once per solve).  On data whose outliers are not
+// sparse (video: every compact-E tile overflows after a few iterations) the
+// compact slots are pure overhead, so after iterations 8 and 24 the dense
+// tiles of the launches since the last check are counted (one host sync) and,
+// at half of all tiles or more, the compact tiles of E^(k) and E^(k-1) are
+// expanded into the dense buffers and K5 runs in its dense-E form from k+1 on.
+// Storage only: the values are the same either way.
+void Session::maybe_dense_e(int k) {
+    if (de_ || de_mode_ != -1 || !de_eligible() || (k != 8 && k != 24)) return;
+    int64_t total = 0, per = 0;
+    counters(&total, &per);
+    const int launches = k - de_prev_k_;
+    const double frac = (launches > 0 && per > 0) ? (double)(total - de_prev_) / ((double)launches * per) : 0.0;
+    de_prev_ = total;
+    de_prev_k_ = k;
+    if (frac < 0.5) return;
+    launch_ce_expand(g_, ce_buf(k), e_buf(k), st_);
+    launch_ce_expand(g_, ce_buf(k - 1), e_buf(k - 1), st_);
+    de_ = true;
 }
 
 void populate_output(void* p, size_t bytes) {
@@ -951,6 +975,7 @@ void Session::run(int iters) {
         }
         mark(5);
         maybe_print(k);
+        maybe_dense_e(k);
     }
     flush_norms();  // the last iteration's stop test (errHist complete after every run)
 }
@@ -1036,7 +1061,7 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
     if (E && g_.n1l > 0) {  // E lives in compact form
         if (f32_)
             launch_ce_expand32(g_, CE_.f(), E_.f(), st_);
-        else
+        else if (!de_)  // (dense-E mode: E^(done) is dense already)
             launch_ce_expand(g_, ce_buf(done), e_buf(done), st_);
     }
     if ((O || E) && g_.n1l > 0) {

@@ -80,9 +80,11 @@ class Session {
     bool is_f32() const { return f32_; }
     void counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch);
     void k5_profile(int* dense_streams, int* slot_accesses) const {
-        *dense_streams = dy_ ? 4 : 6;
-        *slot_accesses = dy_ ? 3 : 2;
+        // dense-E mode: E^(k), E^(k-1) read and E^(k+1) written densely, no slots
+        *dense_streams = de_ ? 7 : (dy_ ? 4 : 6);
+        *slot_accesses = de_ ? 0 : (dy_ ? 3 : 2);
     }
+    bool dense_e() const { return de_; }
     void set_timing(int level);  // 0 off, TRITD_TIMING_ALL, TRITD_TIMING_K5
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
     const std::vector<double>& probe_ms() const { return probe_ms_; }
@@ -185,6 +187,15 @@ class Session {
     // in compact buffer k % 2 (CE_, CE2_) and dense buffer k % 2 (E_, and the
     // pool slot of Y_O, which is not stored in this mode)
     bool dy_ = false;
+    // dense-E mode of K5 (k_admm.hip DE): de_mode_ -1 automatic (switch once E
+    // has turned dense: checked after iterations 8 and 24), 0 never, 1 from the
+    // start (TRITD_DENSE_E); de_prev_* = the dense-tile count at the last check
+    bool de_ = false;
+    int de_mode_ = -1;
+    int64_t de_prev_ = 0;
+    int de_prev_k_ = 0;
+    bool de_eligible() const { return dy_ && !f32_ && !qi_ && g_.RP <= 64; }
+    void maybe_dense_e(int k);
     DBuf CE2_;
     double* ce_buf(int k) const { return (dy_ && (k & 1)) ? CE2_.p : CE_.p; }
     double* e_buf(int k) const { return (dy_ && (k & 1)) ? YO_.p : E_.p; }
