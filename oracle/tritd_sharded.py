@@ -105,11 +105,18 @@ def sharded_admm(D_local, i0, i1, r, opts, A0, B0, C0, allreduce):
     return dict(A_rows=A_loc, B=B, C=C, O=O, E=E, errHist=np.array(errHist), k=k)
 
 
-def k5_workgroups(nl: int, n2: int) -> int:
-    """K5's grid on a shard of nl rows (k_admm.hip k5_grid): one workgroup per
-    4 ij-tiles of 16 padded rows, ij-tile g = (j*n1p + i) // 16."""
+def k5_workgroups(nl: int, n2: int, n3: int = 1, RP: int = 16) -> int:
+    """K5's grid on a shard of nl rows (k_admm.hip k5_grid x k5_tsplit): one
+    workgroup per 4 ij-tiles of 16 padded rows, ij-tile g = (j*n1p + i) // 16,
+    times the chunks of a t-split walk (fp64, RP <= 64: fewer than 256 such
+    workgroups are cut into t-chunks of >= 8 t-tiles, up to ~256 in all)."""
     n1p = -(-nl // 16) * 16
-    return -(-(n1p * n2 // 16) // 4)
+    wg = -(-(n1p * n2 // 16) // 4)
+    ntt = -(-n3 // 16)
+    split = 1
+    if RP <= 64 and wg < 256:
+        split = max(1, min(-(-256 // wg), ntt // 8))
+    return wg * split
 
 
 def library_admm(D_local, i0, i1, r, opts, A0, B0, C0, allreduce, allreduce_max,

@@ -310,7 +310,13 @@ void k5_fused(K5Args a) {
             return;
         }
     }
-    const int64_t bid = (int64_t)blockIdx.x - side;  // this workgroup's group of ij-tiles
+    // workgroup wgi = chunk c of the t-walk (a.tsplit chunks; 1 unless the
+    // problem has too few ij-tiles to fill the GPU, k5_tsplit) x group bid of
+    // 4 ij-tiles
+    const int64_t wgi = (int64_t)blockIdx.x - side;
+    const int64_t ngrp = (a.tiles + K5_WAVES - 1) / K5_WAVES;
+    const int64_t chunk = wgi / ngrp;
+    const int64_t bid = wgi - chunk * ngrp;  // this workgroup's group of ij-tiles
     WT_BEGIN();
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
@@ -332,6 +338,7 @@ void k5_fused(K5Args a) {
     const int64_t j = active ? tile / qper : 0;
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
+    const int64_t t0 = chunk * ntt / a.tsplit, t1 = (chunk + 1) * ntt / a.tsplit;  // this chunk's t-tiles
     // this lane's d2v slot of pair p in t-tile tt: tm_tile_base(tile, tt)/2 + 64p + lane
 
     // C^ rows of one t-tile, staged once per workgroup:
@@ -863,34 +870,35 @@ void k5_fused(K5Args a) {
     xa.edp[0] = xa.edp[1] = xb.edp[0] = xb.edp[1] = d2v{0.0, 0.0};
     xa.ce = xb.ce = xa.cep = xb.cep = 0.0;
     if (!PRO) {
-        load_slot(0, xa);
-        load_slot(1, xb);
+        load_slot(t0, xa);
+        load_slot(t0 + 1, xb);
     }
-    load(0, xa);
-    if (DE || (!PRO && ce_is_dense(xa.ce))) load_dense(0, xa);
-    if (DE || (!PRO && DY && ce_is_dense(xa.cep))) load_dense_p(0, xa);
-    stage(0, 0);
-    if (PIPE) stage(ntt > 1 ? 1 : 0, 1);
+    load(t0, xa);
+    if (DE || (!PRO && ce_is_dense(xa.ce))) load_dense(t0, xa);
+    if (DE || (!PRO && DY && ce_is_dense(xa.cep))) load_dense_p(t0, xa);
+    stage(t0, 0);
+    if (PIPE) stage(t1 - t0 > 1 ? t0 + 1 : t0, 1);
     __syncthreads();
     if (PIPE) xa.l = l_mfma(0);
     xb.l = d4{0.0, 0.0, 0.0, 0.0};
-    int64_t tt = 0;
+    int64_t tt = t0;
     int b = 0;  // buffer of t-tile tt's C^ slice
-    for (; tt + 2 < ntt; tt += 2) {
+    for (; tt + 2 < t1; tt += 2) {
         body(tt, b, xa, xb, true);
         b = bnext(b);
         body(tt + 1, b, xb, xa, true);
         b = bnext(b);
     }
-    if (tt + 1 < ntt) {
+    if (tt + 1 < t1) {
         body(tt, b, xa, xb, true);
         body(tt + 1, bnext(b), xb, xa, false);
     } else {
         body(tt, b, xa, xb, false);
     }
     if (active) {
-        // W^T C/D layout: row k = 16m + tg + 4rr, col ij = il
-        const int64_t wbase = (tile << 4) + il;
+        // W^T C/D layout: row k = 16m + tg + 4rr, col ij = il; a t-split walk
+        // writes its chunk's partial W into set `chunk` (summed by k_w_reduce)
+        const int64_t wbase = (tile << 4) + il + chunk * (int64_t)RP * a.plane;
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -905,7 +913,7 @@ void k5_fused(K5Args a) {
     }
 #endif
     if (!PRO && ndense && lane == 0)  // spread over DENSE_SLOTS counters
-        atomicAdd(a.dense_tiles + ((bid * K5_WAVES + wid) & (DENSE_SLOTS - 1)),
+        atomicAdd(a.dense_tiles + ((wgi * K5_WAVES + wid) & (DENSE_SLOTS - 1)),
                   (unsigned long long)ndense);
     if (!PRO) {
         // fixed-order block reduction of the residual norms
@@ -926,14 +934,39 @@ void k5_fused(K5Args a) {
                 x += red[0][w];
                 y += red[1][w];
             }
-            a.partial[2 * bid] = x;
-            a.partial[2 * bid + 1] = y;
+            a.partial[2 * wgi] = x;
+            a.partial[2 * wgi + 1] = y;
         }
     }
     WT_END(g_wt_k5, PRO ? -1 : bid * K5_WAVES + (threadIdx.x >> 6));
 }
 
 int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }
+
+// t-split of the fp64 K5 walk: a problem with few ij-tiles (the sensor shape
+// 54x4x1152: 16 ij-tiles, 4 workgroups walking 72 t-tiles each) leaves the GPU
+// almost idle, so the walk is cut into chunks of >= 8 t-tiles until there are
+// about 256 workgroups; each chunk's W is a partial sum (k_w_reduce).
+int k5_tsplit(const Geom& g) {
+    if (g.RP > 64) return 1;
+    const int64_t wg = cdiv(g.tiles, K5_WAVES);
+    if (wg >= 256) return 1;
+    int64_t s = cdiv(256, wg);
+    if (s > g.ntt / 8) s = g.ntt / 8;
+    return (int)(s < 1 ? 1 : s);
+}
+
+// Wk (set 0) = sum of the t-split partial sets, in chunk order
+__global__ __launch_bounds__(256) void k_w_reduce(double* Wk, int64_t stride, int sets,
+                                                  const int* stop) {
+    if (*stop) return;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < stride;
+         e += (int64_t)gridDim.x * 256) {
+        double s = Wk[e];
+        for (int c = 1; c < sets; ++c) s += Wk[c * stride + e];
+        Wk[e] = s;
+    }
+}
 
 #if K5_PROF
 }  // namespace tritd
@@ -952,17 +985,19 @@ void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream
     if (a.side.on && (prologue || g.RP > 64)) throw Error(TRITD_ERR_ARG, "K5 side solve: RP <= 64 only");
     if (dense_e && (prologue || !dy || g.RP > 64))
         throw Error(TRITD_ERR_ARG, "K5 dense-E mode: derived-Y_O update, RP <= 64");
-    const dim3 grid(k5_grid(g) + (a.side.on ? 1 : 0)), block(64 * K5_WAVES);
+    K5Args b = a;  // (the macro below launches with `b`)
+    b.tsplit = k5_tsplit(g);
+    const dim3 grid(k5_grid(g) * b.tsplit + (a.side.on ? 1 : 0)), block(64 * K5_WAVES);
 #define K5_CASE(RPV)                                                                       \
     case RPV:                                                                              \
         if (prologue)                                                                      \
-            hipLaunchKernelGGL((k5_fused<RPV, true, false>), grid, block, 0, st, a);       \
+            hipLaunchKernelGGL((k5_fused<RPV, true, false>), grid, block, 0, st, b);       \
         else if (dy && dense_e && RPV <= 64)                                               \
-            hipLaunchKernelGGL((k5_fused<RPV, false, true, (RPV <= 64)>), grid, block, 0, st, a); \
+            hipLaunchKernelGGL((k5_fused<RPV, false, true, (RPV <= 64)>), grid, block, 0, st, b); \
         else if (dy)                                                                       \
-            hipLaunchKernelGGL((k5_fused<RPV, false, true>), grid, block, 0, st, a);       \
+            hipLaunchKernelGGL((k5_fused<RPV, false, true>), grid, block, 0, st, b);       \
         else                                                                               \
-            hipLaunchKernelGGL((k5_fused<RPV, false, false>), grid, block, 0, st, a);      \
+            hipLaunchKernelGGL((k5_fused<RPV, false, false>), grid, block, 0, st, b);      \
         break;
     switch (g.RP) {
         K5_CASE(16)
@@ -976,6 +1011,12 @@ void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream
     }
 #undef K5_CASE
     TRITD_CHECK_LAUNCH();
+    if (b.tsplit > 1) {
+        const int64_t stride = (int64_t)g.RP * g.plane;
+        hipLaunchKernelGGL(k_w_reduce, dim3((unsigned)std::min<int64_t>(cdiv(stride, 256), 2048)),
+                           dim3(256), 0, st, b.Wk, stride, b.tsplit, b.stop);
+        TRITD_CHECK_LAUNCH();
+    }
 }
 
 // Sum n (x, y) pairs in a fixed order: per-thread strided sums, then a

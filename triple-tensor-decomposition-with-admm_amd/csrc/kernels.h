@@ -56,8 +56,12 @@ struct K5Args {
     // Ah = H (k_qi.hip, rows j*n1p+i), ahj = n1p*RP, Bh = ones, bhj = 0.
     int64_t ahj, bhj;
     SideSolve side;  // RP <= 64, CP model: solve A of the next iteration
+    int tsplit = 1;  // chunks of the t-walk (set by launch_k5: k5_tsplit)
 };
 int k5_grid(const Geom& g);
+// chunks of the fp64 K5's t-walk (1 unless the problem has few ij-tiles); K5
+// then runs k5_grid * k5_tsplit workgroups and W needs k5_tsplit sets
+int k5_tsplit(const Geom& g);
 int k5_parts32(const Geom& g);  // fp32 K5's norm-partial count (its workgroups)
 // dense_e: E kept densely for every tile (no compact slots; dy only, RP <= 64)
 void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st,

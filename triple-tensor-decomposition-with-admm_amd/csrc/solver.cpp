@@ -171,7 +171,8 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
             ++q;
         }
     }
-    Wk_.alloc_bytes((size_t)g_.RP * g_.plane * es_);
+    // W, plus the partial sets of a t-split K5 walk (k5_tsplit; fp64)
+    Wk_.alloc_bytes((size_t)g_.RP * g_.plane * es_ * (f32_ ? 1 : (size_t)k5_tsplit(g_)));
     TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.bytes(), st_));
     if (f32_) ChF_.alloc_bytes((size_t)g_.n3p * g_.RP * sizeof(float));
     for (int q = 0; q < 2; ++q) {

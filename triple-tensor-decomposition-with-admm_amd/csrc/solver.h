@@ -124,7 +124,7 @@ class Session {
     void iterate_fused(int k);
     bool fused_ = false;
     // K5's norm-partial count (its workgroups; the fp32 rank-split K5 has more)
-    int k5n() const { return f32_ ? k5_parts32(g_) : k5_grid(g_); }
+    int k5n() const { return f32_ ? k5_parts32(g_) : k5_grid(g_) * k5_tsplit(g_); }
     // pairs in red1_'s norm-partial tail: the largest k5n() over the ranks
     // (shards of different heights launch different K5 grids, and every rank
     // must all-reduce the same count); set by agree_counts()
