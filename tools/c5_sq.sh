@@ -1,0 +1,15 @@
+#!/bin/bash
+# Config-5 fused update (k5_f32s<256>): SQ issue/wait breakdown in two PMC
+# passes (kernel counters only), summarised by tools/pmc_summary.py
+set -uo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/c5sq; mkdir -p $O
+B="python3 bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1"
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS \
+    --output-format csv -d $O/p1 -o run -- $B > $O/p1.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_INSTS_SALU SQ_WAVES \
+    --output-format csv -d $O/p2 -o run -- $B > $O/p2.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+    --output-format csv -d $O/p3 -o run -- $B > $O/p3.log 2>&1 || exit $?
+python3 tools/pmc_summary.py $O "k5_f32s<256>" "k_m3_32<256" > $O/c5_sq.txt
+cat $O/c5_sq.txt
