@@ -15,6 +15,10 @@ if os.environ.get("AB_CFG", "4") == "5":  # 2048x2048x256 r=16 fp32 (bench.py --
     dd = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
     D, A0, B0, C0 = dd["D"].astype(np.float32, order="F"), dd["A0"], dd["B0"], dd["C0"]
     del dd
+elif os.environ.get("AB_CFG", "4") == "3":  # 240x320x300 r=5 video stand-in (bench.py --config 3)
+    n1, n2, n3, r = 240, 320, 300, 5
+    dd = synth.video_like(n1, n2, n3, r, seed=0, init_seed=123)
+    D, A0, B0, C0 = dd["D"], dd["A0"], dd["B0"], dd["C0"]
 elif os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere
     rng = np.random.default_rng(0)
     D = np.asfortranarray(rng.standard_normal((n, n, n)))
@@ -22,7 +26,7 @@ elif os.environ.get("AB_DATA", "bench") == "noise":  # E dense everywhere
 else:  # the bench workload (low rank + 5 % outliers)
     dd = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
     D, A0, B0, C0 = dd["D"], dd["A0"], dd["B0"], dd["C0"]
-opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
+opts = dict(synth.VIDEO_OPTS if os.environ.get("AB_CFG", "4") == "3" else synth.TRAFFIC_OPTS, maxIter=100)
 res = {v: [] for v in vals}
 for rep in range(reps):
     for v in vals:

@@ -950,10 +950,19 @@ int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }
 int k5_tsplit(const Geom& g) {
     if (g.RP > 64) return 1;
     const int64_t wg = cdiv(g.tiles, K5_WAVES);
-    if (wg >= 256) return 1;
-    int64_t s = cdiv(256, wg);
-    if (s > g.ntt / 8) s = g.ntt / 8;
-    return (int)(s < 1 ? 1 : s);
+    const int64_t smax = g.ntt / 8 > 1 ? g.ntt / 8 : 1;  // chunks of >= 8 t-tiles
+    if (const char* e = std::getenv("TRITD_K5_TSPLIT")) {  // A/B override
+        const int64_t f = std::atoll(e);
+        return (int)(f < 1 ? 1 : (f > g.ntt ? g.ntt : f));
+    }
+    if (wg < 256) {  // too few ij-tiles to fill the GPU: ~256 workgroups
+        const int64_t s = std::min(cdiv(256, wg), smax);
+        return (int)(s < 1 ? 1 : s);
+    }
+    // (Splitting to fill the rounds of 512 workgroups, e.g. config 3's 1 200
+    // = 2.34 rounds, measured slower: K5 0.250 -> 0.261 ms with 2 chunks; the
+    // walks are HBM-bound, so a thin last round still streams at full rate.)
+    return 1;
 }
 
 // Wk (set 0) = sum of the t-split partial sets, in chunk order
