@@ -58,6 +58,35 @@ def test_admm_matches_golden(tritd, orc, name):
     check_solution(orc, got, g, g["k"])
 
 
+@pytest.mark.parametrize("name,env", [
+    # dense-E form of K5 from the first iteration (solver.cpp de_mode_)
+    ("g12x10x8_r2", {"TRITD_DENSE_E": "1"}), ("g12x10x8_r2_stop", {"TRITD_DENSE_E": "1"}),
+    ("g17x16x20_r8", {"TRITD_DENSE_E": "1"}), ("g20x24x18_r5_video", {"TRITD_DENSE_E": "1"}),
+    ("g30_r3", {"TRITD_DENSE_E": "1"}), ("g54x4x96_r5_sensor", {"TRITD_DENSE_E": "1"}),
+    # the t-walk cut into chunks whose partial W sets k_w_reduce sums (k5_tsplit)
+    ("g17x16x20_r8", {"TRITD_K5_TSPLIT": "2"}), ("g30_r3", {"TRITD_K5_TSPLIT": "2"}),
+    ("g20x24x18_r5_video", {"TRITD_K5_TSPLIT": "2"}), ("g54x4x96_r5_sensor", {"TRITD_K5_TSPLIT": "3"}),
+    ("g54x4x96_r5_sensor", {"TRITD_K5_TSPLIT": "3", "TRITD_DENSE_E": "1"}),
+])
+def test_admm_storage_forms_match_golden(tritd, orc, name, env, monkeypatch):
+    """K5's other storage/decomposition forms (dense E, split t-walk), forced
+    on the goldens: the same solution within the same tolerances."""
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    g = load_golden(name)
+    got = tritd.triple_decomp_ADMM(g["D"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                   return_E=True, return_iters=True)
+    check_solution(orc, got, g, g["k"])
+    if "TRITD_DENSE_E" in env:  # the form really ran: K5 reports dense E streams, no slots
+        n1, n2, n3 = g["D"].shape
+        s = tritd.Session(g["r"], g["opts"], g["A0"], g["B0"], g["C0"], n1=n1, n2=n2, n3=n3, D=g["D"],
+                          device=0)
+        s.run(1)
+        s.sync()
+        assert s.k5_profile() == (7, 0)
+        s.close()
+
+
 @pytest.mark.parametrize("name", ["g12x10x8_r2", "g30_r3", "g17x16x20_r8"])
 def test_admm_first_iterations(tritd, orc, name):
     """State after iterations 1 and 2 (localises a divergence)."""
