@@ -102,18 +102,21 @@ struct IterScalars {
 // (<= 5 % nonzero and <= 33 per 256-element tile on the bench workload), so
 // it is kept as one 32-double slot per tile (slot of tile ordinal b =
 // tm_tile_base(g, tt)/256 at CE + 32 b):
-//   words 0..3: bit masks; bit l of word w <=> the element lane l holds as
-//               MFMA C/D register element (p, q) = (w >> 1, w & 1), i.e. the
-//               TM in-tile position 128 p + 2 l + q, is nonzero
-//   words 4..30: the nonzero values, ordered by (w, l); unused words are +0,
-//               and word 31 always is (the decoders point lanes whose element
-//               is zero at it instead of selecting afterwards)
+//   words 0..26:  the nonzero values, ordered by (w, l) (see below)
+//   bytes CE_IDX_BYTE + q (words 27..30): the in-tile position of value q,
+//                 64 w + l for the element lane l holds as MFMA C/D register
+//                 element (p, q) = (w >> 1, w & 1), i.e. the TM in-tile
+//                 position 128 p + 2 l + q
+//   word 31:      the count in its low dword (all ones: dense)
 // A tile with more than CE_CAP nonzeros is stored densely in E (TM) and its
-// slot masks are all ones.  Zeros are stored as +0 (MATLAB's E may hold -0,
-// which is numerically identical in every later use).
+// count is all ones.  Zeros are stored as +0 (MATLAB's E may hold -0, which is
+// numerically identical in every later use).  Decoding scatters the values
+// into a per-wave LDS tile image of CE_IMG doubles (256 + a junk word per lane).
 constexpr int CE_SLOT = 32;
-constexpr int CE_CAP = CE_SLOT - 5;
-constexpr int CE_ZERO = CE_SLOT - 1;  // the always-zero word
+constexpr int CE_CAP = 27;
+constexpr int CE_IDX_BYTE = 8 * CE_CAP;  // 216
+constexpr int CE_CNT_WORD = 31;
+constexpr int CE_IMG = 256 + 64;
 
 __host__ __device__ inline int64_t tm_tile_base(int64_t g, int64_t tt, int64_t ntt) {
     return ((((g >> 2) * ntt + tt) << 2) + (g & 3)) << 8;

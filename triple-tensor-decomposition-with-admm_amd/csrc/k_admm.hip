@@ -70,9 +70,6 @@ static constexpr int K5_WAVES = 4;
 #ifndef K5_SWID
 #define K5_SWID 1
 #endif
-#ifndef K5_SMASK
-#define K5_SMASK 0
-#endif
 #ifndef K5_CSIGN
 #define K5_CSIGN 2
 #endif
@@ -170,14 +167,6 @@ __device__ __forceinline__ uint64_t ce_word(double sv, int w) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(__double2hiint(sv), w);
     return ((uint64_t)hi << 32) | lo;
 }
-// Mask word w of the compact-E slot at `slot` through the scalar cache (read
-// only: a uniform address in the constant address space becomes s_load; the
-// kernel later overwrites E^(k-1)'s slot by vector stores but never reads it
-// again, and the scalar cache is invalidated at every kernel start)
-__device__ __forceinline__ uint64_t smask(const double* slot, int w) {
-    typedef const __attribute__((address_space(4))) uint64_t cu64;
-    return ((cu64*)(slot))[w];
-}
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -192,44 +181,41 @@ __device__ __forceinline__ bool lane_bit(uint64_t m, int lane) {
     return (m >> lane) & 1;
 #endif
 }
-// A dense (overflowed) tile has all four mask words set; a stored tile has at
-// most CE_CAP < 64 nonzeros, so mask word 0 alone decides (2 readlanes, not 8)
-__device__ __forceinline__ bool ce_is_dense(double sv) { return ce_word(sv, 0) == ~0ull; }
-// This lane's 4 elements (register order r = 2p+q) from its slot double sv
-// (lane l holds slot word l & 31).  Returns true for a dense (overflowed)
-// tile, whose values are in E instead.
-__device__ __forceinline__ bool ce_decode_m(double sv, int lane, const uint64_t (&m)[4],
-                                            double (&e)[4]);
-__device__ __forceinline__ bool ce_decode(double sv, int lane, double (&e)[4]) {
-    uint64_t m[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) m[w] = ce_word(sv, w);
-    return ce_decode_m(sv, lane, m, e);
+// Compact-E slot (common.h: CE): words 0..26 the nonzero values, bytes
+// CE_IDX_BYTE + q their in-tile positions 64 w + l (element w of lane l, the
+// register order), word CE_CNT_WORD the count (low dword; all ones: dense).
+// A lane holds slot word lane & 31.
+__device__ __forceinline__ bool ce_is_dense(double sv) {
+    return (uint32_t)__builtin_amdgcn_readlane(__double2loint(sv), CE_CNT_WORD) == 0xFFFFFFFFu;
 }
-// the same with the slot's four mask words already in SGPRs
-__device__ __forceinline__ bool ce_decode_m(double sv, int lane, const uint64_t (&m)[4],
-                                            double (&e)[4]) {
-    const int svlo = __double2loint(sv), svhi = __double2hiint(sv);
-    const bool dense = m[0] == ~0ull;  // ce_is_dense
-    int pre = 4;
+// This lane's 4 elements (register order) of the tile whose slot word is sv,
+// through the wave's LDS tile image img (CE_IMG doubles, all zero on entry and
+// on return): lane q < count writes its own value (word q) at its position,
+// every lane reads its four, and the writers zero their position again.  No
+// mask walk: the position byte comes from one lane-constant ds_bpermute pair.
+// Returns true for a dense (overflowed) tile, whose values are in E instead.
+__device__ __forceinline__ bool ce_decode(double sv, int lane, double* img, double (&e)[4]) {
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(__double2loint(sv), CE_CNT_WORD);
+    const int q = lane & 31;
+    const int src = (CE_IDX_BYTE / 8 + (q >> 3)) << 2;  // slot word holding byte q (lane-constant)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, __double2loint(sv));
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, __double2hiint(sv));
+    const int pos = (int)__builtin_amdgcn_ubfe((q & 4) ? hi : lo, 8 * (q & 3), 8);
+    // cnt <= CE_CAP < 32 unless dense (all ones), so lanes >= 32 never write
+    const int at = ((uint32_t)lane < cnt && cnt <= (uint32_t)CE_CAP) ? pos : 256 + lane;
+    img[at] = sv;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        // a lane whose element is zero (and every lane of a dense tile, whose
-        // values come from E) reads the slot's always-zero word: one select
-        // on the source lane instead of two on the value; a stored tile's
-        // sources stay below CE_ZERO, so no wrap either
-        const uint64_t mw = dense ? 0ull : m[w];  // wave-uniform (SALU)
-        const int src = lane_bit(mw, lane) ? pre + lanes_below(mw) : CE_ZERO;
-        const int vlo = __builtin_amdgcn_ds_bpermute(src << 2, svlo);
-        const int vhi = __builtin_amdgcn_ds_bpermute(src << 2, svhi);
-        e[w] = __hiloint2double(vhi, vlo);
-        pre += __builtin_popcountll(mw);
-    }
-    return dense;
+    for (int w = 0; w < 4; ++w) e[w] = img[64 * w + lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    img[at] = 0.0;
+    return cnt == 0xFFFFFFFFu;
 }
 // Store this lane's 4 elements of E (register order) as the tile's slot at
-// CE + sb, or densely into E2 at d2v offset o when they do not fit.  cs: the
-// wave's 96-double LDS scratch (slot image + a junk area for the zeros).
+// (rs, soff), or densely into E2 at d2v offset o when they do not fit.  cs:
+// the wave's 96-double LDS scratch (slot image + a junk area for the zeros).
 // Branch-free: a branch here makes the compiler's vmcnt waits drain the
 // prefetch.
 __device__ __forceinline__ void ce_encode_r(const double (&En)[4], int lane, double* cs,
@@ -253,23 +239,24 @@ __device__ __forceinline__ void ce_encode_r(const double (&En)[4], int lane, dou
     }
     const int l = lane & 31;
     const bool dense = cnt > CE_CAP;
-    // slot image: zeros, then the packed values, then the masks (all lanes
-    // write the same mask words: no lane test)
-    cs[l < 4 ? 32 + lane : l] = 0.0;
+    // slot image: zeros (lanes >= 32 zero their junk word), then the values
+    // and their position bytes, then the count
+    cs[lane < 32 ? lane : lane + 32] = 0.0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    int pre = 4;
+    unsigned char* cb = reinterpret_cast<unsigned char*>(cs);
+    int pre = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        // (a dense tile's image is not used: its values go to the junk area,
-        // they would index past the scratch)
-        const int bit = (!dense && lane_bit(nz[w], lane)) ? 1 : 0;
+        // (a dense tile's image is not used: its values and bytes go to the
+        // lane's junk word)
+        const bool bit = !dense && lane_bit(nz[w], lane);
         const int at = pre + lanes_below(nz[w]), away = 32 + lane;
-        cs[away + ((at - away) & -bit)] = En[w];
+        cs[bit ? at : away] = En[w];
+        cb[bit ? CE_IDX_BYTE + at : 8 * away + w] = (unsigned char)(64 * w + lane);
         pre += __builtin_popcountll(nz[w]);
     }
-#pragma unroll
-    for (int w = 0; w < 4; ++w) cs[w] = __longlong_as_double(dense ? -1ll : (long long)nz[w]);
+    if (lane == 0) cs[CE_CNT_WORD] = __longlong_as_double(dense ? 0xFFFFFFFFll : (long long)cnt);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const double v = cs[l];
@@ -282,8 +269,7 @@ __device__ __forceinline__ void ce_encode_r(const double (&En)[4], int lane, dou
         ++ndense;  // wave-uniform; one atomic per wave at the end (a per-tile
                    // atomic on one counter serialised: 17 -> 53 ms once E turned dense)
     }
-    const double sv = (dense && l >= 4) ? 0.0 : v;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, sv), rs, lane < 32 ? l * 8 : OOB,
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rs, lane < 32 ? l * 8 : OOB,
                                           soff, 0);
 }
 
@@ -470,10 +456,21 @@ void k5_fused(K5Args a) {
     };
     __shared__ double csm[K5_WAVES][96];
     double* cs = csm[wid];
+    // compact-E decode images (ce_decode), zero between uses: one per slot
+    // stream (E^(k), E^(k-1) with dy) where the LDS allows, else shared
+    constexpr int NIMG = (DE || PRO) ? 0 : ((DY && RP <= 64) ? 2 : 1);
+    __shared__ double cimg[NIMG > 0 ? K5_WAVES * NIMG : 1][CE_IMG];
+    double* img = cimg[NIMG > 0 ? wid * NIMG : 0];
+    double* imgp = cimg[NIMG > 1 ? wid * NIMG + 1 : (NIMG > 0 ? wid * NIMG : 0)];
+    if constexpr (NIMG > 0) {
+        for (int e = lane; e < NIMG * CE_IMG; e += 64) img[e] = 0.0;  // (imgp follows img)
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
     // every __shared__ array of this kernel, in bytes (160 KiB per CU; RP =
     // 256 at one wave per SIMD is the largest: ~147 KB)
     constexpr size_t LDS_BYTES =
-        sizeof(double) * (NB * RP * SK + NB * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
+        sizeof(double) * (NB * RP * SK + NB * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 + (NIMG > 0 ? K5_WAVES * NIMG : 1) * CE_IMG +
                           2 * K5_WAVES + (K5_KRLDS ? K5_WAVES * KS * 64 : 0));
     static_assert(LDS_BYTES <= 160 * 1024, "k5_fused: LDS over the 160 KiB of a CU");
 #if K5_BUF
@@ -576,16 +573,8 @@ void k5_fused(K5Args a) {
         // prefetch first; it only needs tile tt+1's dense flag, whose slot
         // arrived with the batch of this tile
         if (pf) {
-#if K5_SMASK
-            // mask word 0 of tile tt+1's slots by scalar loads (uniform address;
-            // the slot lines are in L2 since the vector slot load of a step ago)
-            const int64_t sn = (tm_tile_base(tile, phys(tt + 1), ntt) >> 8) * CE_SLOT;
-            const bool dn1 = PRO ? false : smask(a.CE + sn, 0) == ~0ull;
-            const bool dnp1 = (PRO || !DY) ? false : smask(a.CEp + sn, 0) == ~0ull;
-#else
             const bool dn1 = PRO ? false : ce_is_dense(nx.ce);
             const bool dnp1 = (PRO || !DY) ? false : ce_is_dense(nx.cep);
-#endif
             stage_load(PIPE ? (tt + 2 < ntt ? tt + 2 : ntt - 1) : tt + 1);
             load(tt + 1, nx);
             if constexpr (DE) {  // both E tiles are part of the regular batch
@@ -613,15 +602,7 @@ void k5_fused(K5Args a) {
                     evp[2 * p + q] = cx.edp[p][q];
                 }
         } else if (!PRO) {
-#if K5_SMASK
-            const int64_t sc0 = (tb >> 8) * CE_SLOT;
-            uint64_t mk[4];
-#pragma unroll
-            for (int w = 0; w < 4; ++w) mk[w] = smask(a.CE + sc0, w);
-            const bool dn = ce_decode_m(cx.ce, lane, mk, ev);
-#else
-            const bool dn = ce_decode(cx.ce, lane, ev);
-#endif
+            const bool dn = ce_decode(cx.ce, lane, img, ev);
 #if K5_DNBR
             if (dn) {  // wave-uniform and rare: a scalar branch, not 8 selects
                 asm volatile("" ::: "memory");  // keeps it a branch (no if-conversion)
@@ -639,14 +620,7 @@ void k5_fused(K5Args a) {
             ev[3] = dn ? cx.ed[1][1] : ev[3];
 #endif
             if (DY) {
-#if K5_SMASK
-                uint64_t mp[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) mp[w] = smask(a.CEp + sc0, w);
-                const bool dp = ce_decode_m(cx.cep, lane, mp, evp);
-#else
-                const bool dp = ce_decode(cx.cep, lane, evp);
-#endif
+                const bool dp = ce_decode(cx.cep, lane, imgp, evp);
 #if K5_DNBR
                 if (dp) {
                     asm volatile("" ::: "memory");
@@ -1245,9 +1219,14 @@ __global__ __launch_bounds__(256) void k_ce_expand(const double* __restrict__ CE
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= ntiles) return;
+    __shared__ double cimg[4][CE_IMG];
+    double* img = cimg[threadIdx.x >> 6];
+    for (int e = lane; e < CE_IMG; e += 64) img[e] = 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const double sv = CE[b * CE_SLOT + (lane & 31)];
     double e[4];
-    if (ce_decode(sv, lane, e)) return;  // dense tile: E already holds it
+    if (ce_decode(sv, lane, img, e)) return;  // dense tile: E already holds it
     d2v* E2 = reinterpret_cast<d2v*>(E) + b * 128 + lane;
     E2[0] = d2v{e[0], e[1]};
     E2[64] = d2v{e[2], e[3]};
