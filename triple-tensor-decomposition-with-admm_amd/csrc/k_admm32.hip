@@ -40,7 +40,14 @@ namespace tritd {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 static constexpr int K5W = 4;
-constexpr int CE32_CAP = CE32_SLOT - 8;
+// Compact-E slot (fp32): words 0..49 the nonzero values in (w, l) order,
+// bytes CE32_IDX_BYTE + q (words 50..62) their tile positions 4 l + w (the f4
+// order a lane holds), word 63 the count (all ones: dense).  Decoding
+// scatters the values into a per-wave LDS tile image (k_admm.hip: ce_decode).
+constexpr int CE32_CAP = 50;
+constexpr int CE32_IDX_BYTE = 4 * CE32_CAP;  // 200
+constexpr int CE32_CNT_WORD = 63;
+constexpr int CE32_IMG = 256 + 64;
 
 bool rp_supported32(int RP) {
     return RP == 16 || RP == 32 || RP == 48 || RP == 64 || RP == 128 || RP == 256;
@@ -61,34 +68,34 @@ __device__ __forceinline__ int lanes_below32(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ uint64_t ce32_word(float sv, int w) {
-    const int b = __float_as_int(sv);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(b, 2 * w);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(b, 2 * w + 1);
-    return ((uint64_t)hi << 32) | lo;
+__device__ __forceinline__ bool ce32_is_dense(float sv) {
+    return (uint32_t)__builtin_amdgcn_readlane(__float_as_int(sv), CE32_CNT_WORD) == 0xFFFFFFFFu;
 }
-// a stored slot holds <= CE32_CAP < 64 nonzeros: mask word 0 is all ones only
-// for a dense tile (2 readlanes, not 8; k_admm.hip)
-__device__ __forceinline__ bool ce32_is_dense(float sv) { return ce32_word(sv, 0) == ~0ull; }
 __device__ __forceinline__ bool lane_bit32(uint64_t m, int lane) {
     (void)lane;
     return __builtin_amdgcn_inverse_ballot_w64(m);  // the uniform mask as the lane condition
 }
-// this lane's 4 elements from its slot word sv; true for a dense tile
-__device__ __forceinline__ bool ce32_decode(float sv, int lane, float (&e)[4]) {
-    uint64_t m[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) m[w] = ce32_word(sv, w);
+// this lane's 4 elements from its slot word sv through the wave's LDS tile
+// image img (CE32_IMG floats, zero on entry and on return): lane q < count
+// writes value q at its position, every lane reads its f4, the writers zero
+// their position again; true for a dense tile
+__device__ __forceinline__ bool ce32_decode(float sv, int lane, float* img, float (&e)[4]) {
     const int b = __float_as_int(sv);
-    int pre = 8;
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(b, CE32_CNT_WORD);
+    const int src = (CE32_IDX_BYTE / 4 + (lane >> 2)) << 2;  // word holding byte `lane` (lane-constant)
+    const uint32_t wd = (uint32_t)__builtin_amdgcn_ds_bpermute(src, b);
+    const int pos = (int)__builtin_amdgcn_ubfe(wd, 8 * (lane & 3), 8);
+    const int at = ((uint32_t)lane < cnt && cnt <= (uint32_t)CE32_CAP) ? pos : 256 + lane;
+    img[at] = sv;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const f4 v = *reinterpret_cast<const f4*>(img + 4 * lane);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    img[at] = 0.0f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int src = (pre + lanes_below32(m[w])) & 63;
-        const int v = __builtin_amdgcn_ds_bpermute(src << 2, b);
-        e[w] = lane_bit32(m[w], lane) ? __int_as_float(v) : 0.0f;
-        pre += __builtin_popcountll(m[w]);
-    }
-    return m[0] == ~0ull;  // ce32_is_dense
+    for (int w = 0; w < 4; ++w) e[w] = v[w];
+    return cnt == 0xFFFFFFFFu;
 }
 // store this lane's 4 elements as the tile's slot (every lane one word), or
 // densely (wave-uniform, rare) when they do not fit.  cs: 128-float per-wave
@@ -104,23 +111,20 @@ __device__ __forceinline__ void ce32_encode(const float (&En)[4], int lane, floa
         cnt += __builtin_popcountll(nz[w]);
     }
     const bool dense = cnt > CE32_CAP;
-    cs[lane < 8 ? 64 + lane : lane] = 0.0f;
+    cs[lane] = 0.0f;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    int pre = 8;
+    unsigned char* cb = reinterpret_cast<unsigned char*>(cs);
+    int pre = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        const int bit = (!dense && lane_bit32(nz[w], lane)) ? 1 : 0;
+        const bool bit = !dense && lane_bit32(nz[w], lane);
         const int at = pre + lanes_below32(nz[w]), away = 64 + lane;
-        cs[away + ((at - away) & -bit)] = En[w];
+        cs[bit ? at : away] = En[w];
+        cb[bit ? CE32_IDX_BYTE + at : 4 * away + w] = (unsigned char)(4 * lane + w);
         pre += __builtin_popcountll(nz[w]);
     }
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const uint64_t mw = dense ? ~0ull : nz[w];
-        cs[2 * w] = __int_as_float((int)(uint32_t)mw);
-        cs[2 * w + 1] = __int_as_float((int)(uint32_t)(mw >> 32));
-    }
+    if (lane == 0) cs[CE32_CNT_WORD] = __int_as_float(dense ? -1 : cnt);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const float v = cs[lane];
@@ -129,7 +133,7 @@ __device__ __forceinline__ void ce32_encode(const float (&En)[4], int lane, floa
         ++ndense;  // wave-uniform; one atomic per wave at the end (a per-tile
                    // atomic on one counter serialised: 17 -> 53 ms once E turned dense)
     }
-    slot[lane] = (dense && lane >= 8) ? 0.0f : v;
+    slot[lane] = v;
 }
 
 // Register budget: two waves per SIMD up to RP = 128; at RP = 256 the L
@@ -171,11 +175,18 @@ void k5_f32(K5Args32 a) {
     __shared__ __attribute__((aligned(16))) float sC[2][16 * LDC];
     __shared__ float tsm[K5W][16 * 17]; // per-wave T transpose
     __shared__ float csm[K5W][128];     // per-wave compact-E slot image
+    __shared__ __attribute__((aligned(16))) float cimg[PRO ? 1 : K5W][CE32_IMG];  // decode images
     float* ts = tsm[wid];
     float* cs = csm[wid];
+    if (!PRO) {
+        for (int q = lane; q < CE32_IMG; q += 64) cimg[wid][q] = 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
     // every __shared__ array of this kernel (sC, tsm, csm, the W exchange wl,
     // red), in bytes: at most the 160 KiB of a CU
-    static_assert(sizeof(float) * (2 * 16 * LDC + K5W * 16 * 17 + K5W * 128 + K5W * (RP * 16 + 16)) +
+    static_assert(sizeof(float) * (2 * 16 * LDC + K5W * 16 * 17 + K5W * 128 + K5W * (RP * 16 + 16) +
+                                   (PRO ? 1 : K5W) * CE32_IMG) +
                           sizeof(double) * 2 * K5W <=
                       160 * 1024,
                   "k5_f32: LDS over the 160 KiB of a CU");
@@ -261,7 +272,7 @@ void k5_f32(K5Args32 a) {
         }
         float ev[4];
         if (!PRO) {
-            const bool dn = K5F_EXP == 3 ? false : ce32_decode(cx.ce, lane, ev);
+            const bool dn = K5F_EXP == 3 ? false : ce32_decode(cx.ce, lane, cimg[PRO ? 0 : wid], ev);
             if (K5F_EXP == 3) ev[0] = ev[1] = ev[2] = ev[3] = cx.ce;
 #pragma unroll
             for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
@@ -479,8 +490,12 @@ void k5_f32s(K5Args32 a) {
     __shared__ __attribute__((aligned(16))) float sC[NSL][16 * LDC];
     __shared__ float tsm[2][DEFER ? 2 : 1][16 * 17];
     __shared__ float csm[2][128];
+    __shared__ __attribute__((aligned(16))) float cimg[4][CE32_IMG];  // per-wave decode images
     __shared__ __attribute__((aligned(16))) f4 lx[2][2][64];  // [slot][half] partial L
     float* cs = csm[slot];
+    for (int q = lane; q < CE32_IMG; q += 64) cimg[wid][q] = 0.0f;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     constexpr int WS = RP * 16 + 16;
     static_assert(2 * WS <= 2 * 16 * LDC, "k5_f32s: the W exchange reuses the C^ slices");
 
@@ -581,7 +596,7 @@ void k5_f32s(K5Args32 a) {
             }
             float ev[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             if (CHAIN) {
-                const bool dn = ce32_decode(cx.ce, lane, ev);
+                const bool dn = ce32_decode(cx.ce, lane, cimg[wid], ev);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
                 if (pf) load_slot(tt + 2, cx.ce);
@@ -933,8 +948,13 @@ __global__ __launch_bounds__(256) void k_ce_expand32(const float* __restrict__ C
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= ntiles) return;
+    __shared__ __attribute__((aligned(16))) float cimg[4][CE32_IMG];
+    float* img = cimg[threadIdx.x >> 6];
+    for (int q = lane; q < CE32_IMG; q += 64) img[q] = 0.0f;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     float e[4];
-    if (ce32_decode(CE[b * CE32_SLOT + lane], lane, e)) return;  // dense: E holds it
+    if (ce32_decode(CE[b * CE32_SLOT + lane], lane, img, e)) return;  // dense: E holds it
     reinterpret_cast<f4*>(E)[b * 64 + lane] = f4{e[0], e[1], e[2], e[3]};
 }
 
