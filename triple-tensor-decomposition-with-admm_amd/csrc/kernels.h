@@ -236,7 +236,7 @@ struct K5Args32 {
     const int* stop;
     unsigned long long* dense_tiles;
 };
-constexpr int CE32_SLOT = 64;  // floats per compact-E slot (8 mask words + 56 values)
+constexpr int CE32_SLOT = 64;  // floats per compact-E slot (50 values, their position bytes, the count)
 bool rp_supported32(int RP);
 int padded_rank32(int R);
 void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st);
