@@ -14,9 +14,9 @@
 // T(ij = 4s + (l>>4), t = l & 15) at float 4l + s.
 //
 // Compact E (fp32): one 64-float (256 B) slot per tile, lane l holding word
-// l: words 0..7 are the four 64-bit ballot masks (mask w <=> register element
-// w of every lane), words 8..63 the nonzeros in (w, lane) order; more than 56
-// nonzeros -> the tile is stored densely in E and its masks are all ones.
+// l: words 0..49 the nonzeros in (w, lane) order, bytes 200..249 their tile
+// positions 4 lane + w, word 63 the count; more than 50 nonzeros -> the tile
+// is stored densely in E and its count is all ones (ce32_decode below).
 #include <cstdlib>
 #include <type_traits>
 
