@@ -162,11 +162,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, int b
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes,
                                              0x00020000);
 }
-__device__ __forceinline__ uint64_t ce_word(double sv, int w) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(__double2loint(sv), w);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(__double2hiint(sv), w);
-    return ((uint64_t)hi << 32) | lo;
-}
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
