@@ -150,6 +150,123 @@ def pmc_traffic(config):
     return d.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def primitives(device, n=512, r=8, reps=10):
+    """The API-level kernels north_star prices against the roofline — unfold
+    (unfold.m:6-10, modes 2 and 3), soft_threshold (soft_threshold.m:2) at
+    >= 80 % of HBM, and triple_product (triple_product.m:6, called by both
+    drivers after the solve) on f64 MFMA — on device-resident n^3 fp64 arrays,
+    timed with HIP events on the stream they are launched on."""
+    import ctypes as C
+    import torch
+    from tritd._lib import check, lib
+    dev = torch.device("cuda", device)
+    st = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(st.cuda_stream)
+    N = n ** 3
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(N, dtype=torch.float64, device=dev, generator=g)
+    Y = torch.empty_like(X)
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+
+    def timed(fn, warm=3):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / reps
+
+    out = {"shape": [n, n, n], "r": r, "reps": reps}
+
+    def rec(name, ms, nbytes=None, flops=None):
+        d = {"ms": ms}
+        if nbytes is not None:
+            d["algorithmic_bytes"] = nbytes
+            d["GBs"] = nbytes / ms / 1e6
+            d["hbm_frac"] = d["GBs"] / HBM_PEAK_GBS
+        if flops is not None:
+            d["TFs"] = flops / ms / 1e9
+            d["mfma_frac"] = d["TFs"] / F64_MFMA_PEAK_TFS
+        out[name] = d
+
+    for mode in (2, 3):
+        ms = timed(lambda: check(lib.tritd_dev_unfold_f64(p(X), n, n, n, mode, p(Y), sp)))
+        rec("unfold_mode%d" % mode, ms, 2 * N * 8)
+    ms = timed(lambda: check(lib.tritd_dev_soft_threshold_f64(p(X), N, C.c_double(0.5), p(Y), sp)))
+    rec("soft_threshold", ms, 2 * N * 8)
+    R = r * r
+    A = torch.randn(n * R, dtype=torch.float64, device=dev, generator=g)
+    B = torch.randn(R * n, dtype=torch.float64, device=dev, generator=g)
+    Cc = torch.randn(R * n, dtype=torch.float64, device=dev, generator=g)
+    ms = timed(lambda: check(lib.tritd_dev_triple_product_f64(p(A), p(B), p(Cc), n, n, n, r, p(Y),
+                                                             sp)))
+    rec("triple_product", ms, N * 8, 2.0 * N * R)
+    del X, Y, A, B, Cc
+    torch.cuda.empty_cache()
+    return out
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N > 1` without a torch.distributed launcher around us: start
+    the N rank processes ourselves, as CHILD processes (never an exec; this
+    process has not touched the GPU), with the environment torchrun would give
+    them (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT on 127.0.0.1).  Exit
+    code: 0 only if every rank exits 0; the first failure stops the rest."""
+    import signal
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                for q in live:  # a failed rank would leave the others in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def launch_check(args):
+    """--launch-check: the rank plumbing alone (gloo, no GPU): every rank joins
+    the process group, the ranks count themselves with an all-reduce, rank 0
+    prints one JSON line.  CPU test of the `--gpus N` spawn path."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_counted": int(t.item()),
+                          "gpus_arg": args.gpus}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,21 +279,33 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end one-shot calls")
+    ap.add_argument("--no-prims", action="store_true", help="skip the primitive kernels")
     ap.add_argument("--comm", default="rccl", choices=("rccl", "host"),
                     help="N > 1: libtritd's RCCL communicator (default), or the host all-reduce "
                          "transport over gloo (correctness rehearsal with ranks sharing a GPU)")
     # --algo als: triple_decomp_ALS.m on the config-4 workload
     ap.add_argument("--algo", default="admm", choices=("admm", "als"))
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test the N-rank launch only (gloo, no GPU work)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # never a silent one-rank run of an N-GPU request
+        return spawn_ranks(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d does not match WORLD_SIZE %d" % (args.gpus, world))
+    if args.launch_check:
+        return launch_check(args)
     if args.algo == "als":
+        if world > 1:
+            raise SystemExit("--algo als runs on one GPU")
         return bench_als(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     host_comm = args.comm == "host"
-    if world != args.gpus and world > 1:
-        raise SystemExit("--gpus must match WORLD_SIZE")
 
     import torch
     dist = None
@@ -231,6 +360,10 @@ def main():
     comm = None
     if world > 1:
         comm = (make_host_comm if host_comm else make_comm)(dist, rank, world, local_rank)
+    # what the library's communicator itself reports (RCCL: ncclCommCount)
+    comm_info = comm.info() if comm is not None else (1, 0, "none")
+    if comm is not None and comm_info[0] != world:
+        raise SystemExit("communicator reports %d ranks, WORLD_SIZE is %d" % (comm_info[0], world))
 
     # inputs resident in HBM before the timed region
     dev = torch.device("cuda", local_rank)
@@ -349,6 +482,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = end_to_end(tritd, D, r, opts, data["A0"], data["B0"], data["C0"], local_rank)
 
+    prims = None
+    if rank == 0 and world == 1 and not args.no_prims:
+        prims = primitives(local_rank)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], cpu_iters)
@@ -374,6 +511,8 @@ def main():
                        "parallelism": "mode1-shard x%d" % world
                                       + (" (host all-reduce rehearsal: not a scaling number)"
                                          if host_comm and world > 1 else "")},
+            "comm": {"transport": comm_info[2], "nranks": comm_info[0]},
+            "rccl_nranks": comm_info[0] if comm_info[2] == "rccl" else None,
             "rre_final": rre,
             "k_final": k_final,
             "errHist_final": errhist_final,
@@ -387,6 +526,8 @@ def main():
             # one whole triple_decomp_ADMM call (maxIter=100), host arrays in and out,
             # timed like the drivers' tic/toc (traffic_triple_comparison.m:51,61)
             "end_to_end": e2e,
+            # unfold / soft_threshold / triple_product on 512^3 fp64, device-resident
+            "primitives": prims,
         }
         print(json.dumps(line), flush=True)
 
@@ -481,4 +622,4 @@ def bench_als(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -219,17 +219,24 @@ typedef int32_t (*tritd_allreduce_fn)(double* buf, int64_t count, int32_t op, vo
 tritd_status tritd_comm_create_host(tritd_comm** out, tritd_allreduce_fn fn, void* user,
                                     int32_t nranks, int32_t rank, int32_t device);
 void tritd_comm_destroy(tritd_comm* c);
+/* What the communicator itself reports: for RCCL, ncclCommCount /
+ * ncclCommUserRank read back from the communicator (so a caller can prove
+ * RCCL saw every rank); for the host transport, the values it was created
+ * with.  transport: 0 = RCCL, 1 = host. */
+tritd_status tritd_comm_info(tritd_comm* c, int32_t* nranks, int32_t* rank, int32_t* transport);
 
 /* Device set of the one-shot entry points (the MEX host
- * drives every GPU from its one thread).  With n > 1, tritd_admm_{f64,f32}
- * (device = -1) shard D along mode 1 over the set and run
- * every iteration's phases on all shards from the calling thread; the three
- * reductions per iteration are grouped ncclAllReduce calls over
- * communicators from ncclCommInitAll (distinct devices), cached until the set
- * changes or tritd_shutdown.  One device repeated n times runs n virtual
- * shards on it (in-device sums).  n = 0 clears the set.  Replaces the
- * reference's single-process CPU call (triple_decomp_ADMM.m:1) for data that
- * exceeds one GPU. */
+ * calls from its one thread).  With n > 1, tritd_admm_{f64,f32} (device =
+ * -1) shard D along mode 1 over the set: the library runs one
+ * session per shard with a communicator, each stepped by a library-owned
+ * host thread (shard 0 on the calling thread, so disp prints stay there)
+ * through the same fused two-all-reduce schedule as one process per GPU.
+ * Distinct devices all-reduce over RCCL (communicators from ncclCommInitAll,
+ * cached until the set changes or tritd_shutdown); one device repeated n
+ * times runs n shards on it with an in-process all-reduce.  TRITD_SHOV=0
+ * selects the phase-serial order driven from the calling thread instead.
+ * n = 0 clears the set.  Replaces the reference's single-process CPU call
+ * (triple_decomp_ADMM.m:1) for data that exceeds one GPU. */
 tritd_status tritd_set_devices(const int32_t* devices, int32_t n);
 /* Frees the cached communicators and clears the device set (mexAtExit). */
 void tritd_shutdown(void);

@@ -162,3 +162,30 @@ def test_build_keeps_matlab_rounding_flags():
     for bad in ("-ffast-math", "-fassociative-math", "-Ofast", "-funsafe-math-optimizations",
                 "-ffp-contract=fast", "-ffp-contract=on"):
         assert bad not in mk, bad
+
+
+def test_make_tracks_every_header():
+    """bench.py's ensure_built() trusts `make -q`: every header of csrc/ and the
+    ABI header must be a prerequisite, so an edit to any of them (pinv.h,
+    sweep.h, ...) marks the library out of date."""
+    csrc = os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd", "csrc")
+    if subprocess.run(["make", "-q", "-C", csrc], capture_output=True).returncode != 0:
+        pytest.skip("library not built (or out of date) in this tree")
+    hdrs = [f for f in os.listdir(csrc) if f.endswith(".h")] + ["../../include/tritd.h"]
+    assert "pinv.h" in hdrs and "sweep.h" in hdrs
+    for h in hdrs:
+        p = subprocess.run(["make", "-q", "-W", h, "-C", csrc], capture_output=True)
+        assert p.returncode == 1, "an edit to %s would not rebuild libtritd.so" % h
+
+
+def test_product_reads_few_environment_knobs():
+    """The product path reads a handful of environment knobs, each exercised
+    by a test: TRITD_DENSE_E, TRITD_PROBE, TRITD_K5_TSPLIT,
+    TRITD_FUSED, TRITD_SHOV.  No per-launch experiment switches."""
+    csrc = os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd", "csrc")
+    knobs = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            knobs |= set(re.findall(r'getenv\("(TRITD_\w+)"\)', open(os.path.join(csrc, f)).read()))
+    assert knobs <= {"TRITD_DENSE_E", "TRITD_PROBE", "TRITD_K5_TSPLIT", "TRITD_FUSED", "TRITD_SHOV"}, knobs
+    assert len(knobs) <= 8

@@ -81,6 +81,48 @@ def test_f32_large_rank_vs_c_oracle(tritd, cref, shape, r, iters):
     _compare(tritd, cref, d["D"].astype(np.float32), r, opts, d["A0"], d["B0"], d["C0"])
 
 
+@pytest.mark.timeout(300)
+def test_f32_r16_long_horizon_vs_c_oracle(tritd, cref, capsys):
+    """Config 5's rank (r = 16, padded rank 256) over the whole 100-iteration
+    horizon of the bench, at 256^3 (n_k >= R = 256: well-conditioned Grams)
+    where the C restatement takes ~30 s.  The restatement follows MATLAB's
+    class rules (L = triple_product of double factors, rounded to single where
+    it meets D, triple_product.m:6, triple_decomp_ADMM.m:41,50); the GPU forms
+    L and W on f32 MFMA with f32 accumulation.  This bounds
+    what that deviation does to the solve over the bench's horizon: same k,
+    errHist, L, O, E at the fp32 tolerance, and the driver's RRE against L*
+    (traffic_triple_comparison.m:62-63) within 1e-6 + 2e-5 RRE."""
+    import time
+
+    import tritd_oracle as orc
+    from tritd import synth
+    mod, lib = cref
+    n, r = 256, 16
+    d = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
+    D = d["D"].astype(np.float32, order="F")
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=100)
+    t0 = time.time()
+    ref = mod.admm(lib, D, r, opts, d["A0"], d["B0"], d["C0"])
+    tc = time.time() - t0
+    A, B, C, O, eh, E, k = tritd.triple_decomp_ADMM(D, r, opts, d["A0"], d["B0"], d["C0"],
+                                                    return_E=True, return_iters=True)
+    L = orc.triple_product(A, B, C)
+    Lr = orc.triple_product(ref[0], ref[1], ref[2])
+    nL = np.linalg.norm(d["Lstar"])
+    rre = np.linalg.norm(L - d["Lstar"]) / nL
+    rre_c = np.linalg.norm(Lr - d["Lstar"]) / nL
+    stats = dict(k=k, k_c=ref[6], rel_L=rel(L, Lr), rel_O=rel(O.astype(np.float64), ref[3].astype(np.float64)),
+                 rel_E=rel(E.astype(np.float64), ref[5].astype(np.float64)), rre=rre, rre_c=rre_c,
+                 d_rre=abs(rre - rre_c), eh_last=float(eh[-1]), eh_last_c=float(ref[4][-1]),
+                 max_rel_eh=float(np.max(np.abs(eh - ref[4]) / ref[4])), c_seconds=round(tc, 1))
+    with capsys.disabled():
+        print("  r=16 fp32 long horizon:", stats, flush=True)
+    assert k == ref[6] == 100
+    assert stats["rel_L"] <= TOL and stats["rel_O"] <= TOL and stats["rel_E"] <= TOL
+    np.testing.assert_allclose(eh, ref[4], rtol=1e-3, atol=1e-4 * ref[4][0])
+    assert stats["d_rre"] <= 1e-6 + 2e-5 * rre_c
+
+
 @pytest.mark.parametrize("case", ["mixed_tiles", "all_dense"])
 def test_f32_compact_e_overflow_tiles(tritd, cref, case):
     """Compact E in fp32: 64-word slots, more than 56 nonzeros of a 256-element

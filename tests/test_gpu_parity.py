@@ -110,10 +110,17 @@ def test_virtual_shards_match_golden(tritd, orc, name, P):
     check_solution(orc, got, g, g["k"])
 
 
-@pytest.mark.parametrize("name,P", [("g30_r3", 3), ("g54x4x96_r5_sensor", 2)])
-def test_device_set_matches_golden(tritd, orc, name, P):
-    """tritd_set_devices: one GPU repeated P times drives the
-    sharded schedule of the single-process multi-GPU path from this thread."""
+@pytest.mark.parametrize("name,P,serial", [("g30_r3", 3, False), ("g54x4x96_r5_sensor", 2, False),
+                                           ("g17x16x20_r8", 3, False), ("g12x10x8_r2_stop", 2, False),
+                                           ("g30_r3", 3, True), ("g54x4x96_r5_sensor", 2, True)])
+def test_device_set_matches_golden(tritd, orc, name, P, serial, monkeypatch):
+    """tritd_set_devices: one GPU repeated P times.  Default:
+    one host thread per shard steps a Session with a communicator through the
+    fused two-all-reduce schedule bench.py runs (api.cpp run_group; in-process
+    all-reduce for a repeated device).  TRITD_SHOV=0: the phase-serial order
+    driven from the calling thread (run_group_serial)."""
+    if serial:
+        monkeypatch.setenv("TRITD_SHOV", "0")
     g = load_golden(name)
     tritd.set_devices([0] * P)
     try:

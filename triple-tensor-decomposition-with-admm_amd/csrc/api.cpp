@@ -4,10 +4,14 @@
 // message, and never writes its inputs.
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "als.h"
@@ -202,14 +206,170 @@ struct DeviceGroup {
     }
 };
 
-// One ADMM problem sharded along mode 1 over `devs`: every
-// iteration runs the four phases of solver.cpp on each shard with the three
-// reductions between them.  D, O, E are column-major n1 x n2 x n3 host arrays
-// of es-byte elements.
+// In-process all-reduce of a device group whose shards share a GPU (one
+// device repeated: RCCL refuses a GPU twice in one communicator): the host
+// transport of each shard's session lands here, on that shard's host thread.
+// Sums run in shard order (s = b0; s += b1; ...), like the device-side
+// virtual-shard sum.  abort() wakes every waiter with a failure, so a shard
+// that throws never leaves the others blocked in a collective.
+struct ThreadReducer {
+    struct Rank {
+        ThreadReducer* r;
+        int rank;
+    };
+    int P;
+    std::vector<Rank> ranks;
+    std::vector<double*> bufs;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool aborted = false;
+    explicit ThreadReducer(int p) : P(p), bufs(p, nullptr) {
+        for (int q = 0; q < p; ++q) ranks.push_back({this, q});
+    }
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (aborted) return false;
+        const uint64_t g = gen;
+        if (++arrived == P) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g || aborted; });
+        }
+        return !aborted;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
+    // tritd_allreduce_fn
+    static int32_t allreduce(double* buf, int64_t count, int32_t op, void* user) {
+        Rank* rk = static_cast<Rank*>(user);
+        ThreadReducer* r = rk->r;
+        r->bufs[rk->rank] = buf;
+        if (!r->barrier()) return 1;
+        if (rk->rank == 0) {  // the others wait at the next barrier
+            for (int64_t e = 0; e < count; ++e) {
+                double v = r->bufs[0][e];
+                for (int q = 1; q < r->P; ++q) v = op ? std::fmax(v, r->bufs[q][e]) : v + r->bufs[q][e];
+                for (int q = 0; q < r->P; ++q) r->bufs[q][e] = v;
+            }
+        }
+        return r->barrier() ? 0 : 1;
+    }
+};
+
+// One ADMM problem sharded along mode 1 over `devs`, driven
+// the way one process per GPU drives it: each shard is a Session with a
+// communicator, stepped by its own host thread through the same schedule
+// bench.py and the multi-rank tests run (the fused single-stream iteration
+// with two all-reduces per iteration, or its side-stream form for fp32 / Qi /
+// r > 8).  Distinct devices all-reduce over RCCL (communicators from
+// ncclCommInitAll, cached); one device repeated uses the in-process
+// ThreadReducer.  Shard 0 runs on the calling thread, so `disp` prints (the
+// MEX's mexPrintf) stay on the host's own thread.  D, O, E are column-major
+// n1 x n2 x n3 host arrays of es-byte elements.
+void run_group_serial(const std::vector<int>& devs, const void* D, size_t es, uint32_t flags,
+                      int64_t n1, int64_t n2, int64_t n3, int32_t r, const tritd_opts& o,
+                      const double* A0, const double* B0, const double* C0, double* A, double* B,
+                      double* C, void* O, void* E, double* errHist, int32_t* iters);
+
 void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t flags, int64_t n1,
                int64_t n2, int64_t n3, int32_t r, const tritd_opts& o, const double* A0,
                const double* B0, const double* C0, double* A, double* B, double* C, void* O,
                void* E, double* errHist, int32_t* iters) {
+    {
+        // TRITD_SHOV=0: the phase-serial order of round 1 (one host thread
+        // enqueues every shard's phases, three reductions per iteration)
+        const char* sh = std::getenv("TRITD_SHOV");
+        if (sh && std::atoi(sh) == 0) {
+            run_group_serial(devs, D, es, flags, n1, n2, n3, r, o, A0, B0, C0, A, B, C, O, E,
+                             errHist, iters);
+            return;
+        }
+    }
+    DeviceGroup grp(devs, n1);
+    const int P = grp.size();
+    if (P == 1) {
+        Session s(devs[0], D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, flags);
+        s.run(o.maxIter);
+        int k = 0;
+        s.get(A, B, C, O, E, n1, errHist, &k);
+        g_last_flags |= s.flags();
+        if (iters) *iters = k;
+        return;
+    }
+    std::unique_ptr<ThreadReducer> red;
+    if (grp.same) red.reset(new ThreadReducer(P));
+    std::vector<tritd_comm> comms((size_t)P);
+    for (int p = 0; p < P; ++p) {
+        comms[p].nranks = P;
+        comms[p].rank = p;
+        comms[p].device = devs[p];
+        if (grp.same) {
+            comms[p].host_fn = &ThreadReducer::allreduce;
+            comms[p].host_user = &red->ranks[p];
+        } else {
+            comms[p].comm = g_comms[p];  // owned by the cache (group_comms)
+        }
+    }
+    std::vector<std::exception_ptr> err((size_t)P);
+    std::vector<uint32_t> fl((size_t)P, 0);
+    std::vector<int> kk((size_t)P, 0);
+    bool aborted_rccl = false;
+    std::mutex abort_m;
+    auto abort_all = [&] {
+        if (red) {
+            red->abort();
+            return;
+        }
+        std::lock_guard<std::mutex> lk(abort_m);
+        if (aborted_rccl) return;
+        aborted_rccl = true;
+        // unblocks the other shards' collectives; the communicators are gone
+        for (ncclComm_t c : g_comms)
+            if (c) (void)ncclCommAbort(c);
+        g_comms.clear();
+        g_comm_devs.clear();
+    };
+    auto shard = [&](int p) {
+        try {
+            const auto [i0, i1] = grp.rows(p, n1);
+            TRITD_HIP(hipSetDevice(devs[p]));
+            Session s(devs[p], static_cast<const char*>(D) + i0 * es, n1, n1, n2, n3, i0, i1, r, o,
+                      A0, B0, C0, &comms[p], flags);
+            s.run(o.maxIter);
+            s.get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr,
+                  O ? static_cast<char*>(O) + i0 * es : nullptr,
+                  E ? static_cast<char*>(E) + i0 * es : nullptr, n1, p == 0 ? errHist : nullptr,
+                  &kk[p]);
+            fl[p] = s.flags();
+        } catch (...) {
+            err[p] = std::current_exception();
+            abort_all();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int p = 1; p < P; ++p) th.emplace_back(shard, p);
+    shard(0);
+    for (auto& t : th) t.join();
+    for (int p = 0; p < P; ++p)
+        if (err[p]) std::rethrow_exception(err[p]);
+    for (int p = 0; p < P; ++p) g_last_flags |= fl[p];
+    if (iters) *iters = kk[0];
+}
+
+// The phase-serial schedule (TRITD_SHOV=0): every iteration runs the four
+// phases of solver.cpp on each shard with the three reductions between them.  D, O, E are column-major n1 x n2 x n3 host arrays
+// of es-byte elements.
+void run_group_serial(const std::vector<int>& devs, const void* D, size_t es, uint32_t flags,
+                      int64_t n1, int64_t n2, int64_t n3, int32_t r, const tritd_opts& o,
+                      const double* A0, const double* B0, const double* C0, double* A, double* B,
+                      double* C, void* O, void* E, double* errHist, int32_t* iters) {
     DeviceGroup grp(devs, n1);
     const int P = grp.size();
     std::vector<std::unique_ptr<Session>> ss;
@@ -607,6 +767,21 @@ void tritd_comm_destroy(tritd_comm* c) {
     if (!c) return;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     delete c;
+}
+
+tritd_status tritd_comm_info(tritd_comm* c, int32_t* nranks, int32_t* rank, int32_t* transport) {
+    return guarded([&] {
+        need(c, "comm");
+        int n = c->nranks, me = c->rank;
+        if (c->comm) {
+            ncclResult_t r = ncclCommCount(c->comm, &n);
+            if (r == ncclSuccess) r = ncclCommUserRank(c->comm, &me);
+            if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+        }
+        if (nranks) *nranks = n;
+        if (rank) *rank = me;
+        if (transport) *transport = c->comm ? 0 : 1;
+    });
 }
 
 tritd_status tritd_admm_sharded_virtual_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,

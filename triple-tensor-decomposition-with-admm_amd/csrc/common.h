@@ -67,6 +67,7 @@ struct Geom {
     int64_t ntt = 0;                 // n3p / 16 (t-tiles)
     int64_t tiles4 = 0;              // tiles rounded up to the group of 4
     int64_t Ntm = 0;                 // doubles of one tile-major tensor (tiles4*ntt*256)
+    int tsplit = 1;                  // chunks of K5's t-walk (k5_tsplit, fixed at session creation)
 };
 
 inline Geom make_geom(int64_t n1, int64_t n2, int64_t n3, int64_t i0, int64_t i1, int r) {

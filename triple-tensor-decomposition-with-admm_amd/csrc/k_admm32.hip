@@ -22,20 +22,6 @@
 
 #include "kernels.h"
 
-// K5F_EXP (timing experiments only, results invalid): 1 no W MFMAs, 2 no L
-// MFMAs, 3 no compact-E decode/encode, 4 no C^ staging
-#ifndef K5F_EXP
-#define K5F_EXP 0
-#endif
-// k5_f32s: 0 both waves of a pair run the elementwise chain, 1 only one does,
-// 2 = 1 with the roles alternating between workgroups (round 5, interleaved
-// A/B at config 5: K5 15.73 -> 15.45 ms, iteration 23.72 -> 23.42 ms), 3 = 2
-// with the other wave's W MFMAs deferred by one t-tile (no barrier between
-// the chain and W: K5 15.49 -> 15.24 ms, iteration 22.23 -> 21.95 ms)
-#ifndef K5F_LEAN
-#define K5F_LEAN 3
-#endif
-
 namespace tritd {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -197,7 +183,6 @@ void k5_f32(K5Args32 a) {
     constexpr int NS = (SQ + 64 * K5W - 1) / (64 * K5W);
     f4 sv[NS];
     auto stage_load = [&](int64_t tt) {
-        if (K5F_EXP == 4) return;
         const f4* src = reinterpret_cast<const f4*>(a.ChF + (tt << 4) * RP);
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
@@ -206,7 +191,6 @@ void k5_f32(K5Args32 a) {
         }
     };
     auto stage_store = [&](int buf) {
-        if (K5F_EXP == 4) return;
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int e = threadIdx.x + q * 64 * K5W;
@@ -272,8 +256,7 @@ void k5_f32(K5Args32 a) {
         }
         float ev[4];
         if (!PRO) {
-            const bool dn = K5F_EXP == 3 ? false : ce32_decode(cx.ce, lane, cimg[PRO ? 0 : wid], ev);
-            if (K5F_EXP == 3) ev[0] = ev[1] = ev[2] = ev[3] = cx.ce;
+            const bool dn = ce32_decode(cx.ce, lane, cimg[PRO ? 0 : wid], ev);
 #pragma unroll
             for (int r = 0; r < 4; ++r) ev[r] = dn ? cx.ed[r] : ev[r];
             if (pf) load_slot(tt + 2, cx.ce);
@@ -297,10 +280,7 @@ void k5_f32(K5Args32 a) {
                 const int gl = tg * (KS / 4) + s4;
                 const f4 c = cL[WB ? gran(gl / G, gl % G) : gl];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (K5F_EXP == 2) lacc[u][0] += c[u] * kr[4 * s4 + u];
-                    else lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
-                }
+                for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
             }
             const f4 Lv = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
             float En[4];
@@ -331,8 +311,7 @@ void k5_f32(K5Args32 a) {
             }
             YL4[o] = YLn;
             YO4[o] = YOn;
-            if (K5F_EXP == 3) a.CE[(tb >> 8) * CE32_SLOT + lane] = En[0] + En[1] + En[2] + En[3];
-            else ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), ndense);
+            ce32_encode(En, lane, cs, a.CE + (tb >> 8) * CE32_SLOT, E4 + (tb >> 2), ndense);
         }
         // T -> TX order through the wave's LDS tile: ts[t][ij]
 #pragma unroll
@@ -352,10 +331,7 @@ void k5_f32(K5Args32 a) {
                 for (int q = 0; q < G; ++q) {
                     const f4 c = cW[gran(il, q)];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (K5F_EXP == 1) wacc[4 * q + u][r] += c[u] * tr[r];
-                        else wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
-                    }
+                    for (int u = 0; u < 4; ++u) wacc[4 * q + u] = mfma32(c[u], tr[r], wacc[4 * q + u]);
                 }
             }
         } else {
@@ -363,8 +339,7 @@ void k5_f32(K5Args32 a) {
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
-                    if (K5F_EXP == 1) wacc[m][r] += cR[(4 * tg + r) * LDC + 16 * m + il] * tr[r];
-                    else wacc[m] = mfma32(cR[(4 * tg + r) * LDC + 16 * m + il], tr[r], wacc[m]);
+                    wacc[m] = mfma32(cR[(4 * tg + r) * LDC + 16 * m + il], tr[r], wacc[m]);
         }
         if (pf) stage_store(buf ^ 1);
         __syncthreads();
@@ -451,7 +426,7 @@ void k5_f32(K5Args32 a) {
     }
 }
 
-// RP = 256 with the rank split over a wave pair (K5F_SPLIT, default): two
+// RP = 256 with the rank split over a wave pair (the default there): two
 // waves share each ij-tile, wave h of the pair holding the K-steps
 // s in [h*KS/2, (h+1)*KS/2) of the L operand (k = (l>>4) * KS + s) and the
 // W M-tiles m = 4q + u of granules q in [h*G/2, (h+1)*G/2).  Per t-tile each
@@ -480,15 +455,14 @@ void k5_f32s(K5Args32 a) {
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
     auto gran = [](int c, int q) { return c * G + ((q + ((c * G) >> 4)) & (G - 1)); };
-    // DEFER (LEAN 3): the h = 1 wave runs the W MFMAs of tile tt-1 during
-    // step tt (beside the chain of tt on its partner), from a T transpose
-    // buffer and a C^ slice one step old: no barrier between the chain and W,
-    // three C^ slices (tt-1 in use by h = 1, tt, tt+1 being staged) and two
-    // transpose buffers
-    constexpr bool DEFER = K5F_LEAN >= 3;
-    constexpr int NSL = DEFER ? 3 : 2;
+    // Deferred W: the h = 1 wave runs the W MFMAs of tile tt-1 during step tt
+    // (beside the chain of tt on its partner), from a T transpose buffer and a
+    // C^ slice one step old: no barrier between the chain and W, three C^
+    // slices (tt-1 in use by h = 1, tt, tt+1 being staged) and two transpose
+    // buffers (round 3: K5 15.49 -> 15.24 ms, iteration 22.23 -> 21.95 ms)
+    constexpr int NSL = 3;
     __shared__ __attribute__((aligned(16))) float sC[NSL][16 * LDC];
-    __shared__ float tsm[2][DEFER ? 2 : 1][16 * 17];
+    __shared__ float tsm[2][2][16 * 17];
     __shared__ float csm[2][128];
     __shared__ __attribute__((aligned(16))) float cimg[4][CE32_IMG];  // per-wave decode images
     __shared__ __attribute__((aligned(16))) f4 lx[2][2][64];  // [slot][half] partial L
@@ -541,37 +515,31 @@ void k5_f32s(K5Args32 a) {
     };
     double ssL = 0.0, ssO = 0.0;
     unsigned ndense = 0;
-    // SPLIT (LEAN 4): the pair splits by role instead of by rank: wave h = 0
-    // computes all of L (both K halves, summed in the same order as the
-    // exchange it replaces: results unchanged) and runs the chain; wave h = 1
-    // accumulates all of W, one t-tile late.  No L exchange, so one barrier
-    // per t-tile instead of two; 64 MFMAs per wave per t-tile either way.
-    constexpr bool SPLIT = K5F_LEAN >= 4;
-    static_assert(!SPLIT || DEFER, "k5_f32s: SPLIT builds on DEFER");
-    f4 wacc[SPLIT ? MT : MTH];
+    // (Splitting the pair by role instead — one wave all of L and the chain,
+    // the other all of W — measured 16.03 vs 15.22 ms, round 3.)
+    f4 wacc[MTH];
 
     // the walk, specialised per half (straight-line code in each)
     auto walk = [&](auto HC) {
         constexpr int h = decltype(HC)::value;
-        constexpr int NKR = SPLIT ? (h == 0 ? KS : 0) : KSH;  // KR operands this wave holds
-        constexpr int NWT = SPLIT ? (h == 1 ? MT : 0) : MTH;  // W M-tiles this wave accumulates
-        // KR(ij = l & 15, k = (l>>4) * KS + k0 + s), single-rounded; k0 = h*KSH (rank split) or 0
-        float kr[NKR > 0 ? NKR : 1];
+        constexpr int NKR = KSH;  // KR operands this wave holds
+        constexpr int NWT = MTH;  // W M-tiles this wave accumulates
+        // KR(ij = l & 15, k = (l>>4) * KS + h*KSH + s), single-rounded
+        float kr[NKR];
 #pragma unroll
         for (int s = 0; s < NKR; ++s) {
-            const int k = tg * KS + (SPLIT ? 0 : h * KSH) + s;
+            const int k = tg * KS + h * KSH + s;
             kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
         }
 #pragma unroll
         for (int m = 0; m < NWT; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-        // LEAN: only the h = 0 wave of the pair loads the tile, decodes E and
-        // runs the elementwise chain; the h = 1 wave takes T from the LDS
-        // transpose buffer after one more barrier (its SIMD runs the other
-        // resident wave meanwhile)
-        constexpr bool CHAIN = !K5F_LEAN || h == 0;
+        // only the h = 0 wave of the pair loads the tile, decodes E and runs
+        // the elementwise chain (round 3: K5 15.73 -> 15.45 ms); the h = 1
+        // wave takes T from the LDS transpose buffer a step later
+        constexpr bool CHAIN = h == 0;
         // W^T += C^T T for this half's M-tiles (granules q in [h*GH, (h+1)*GH))
         auto wmfma = [&](const float* cR, const float (&tr)[4]) {
-            constexpr int NQ = NWT / 4, Q0 = SPLIT ? 0 : h * GH;  // granules of this wave
+            constexpr int NQ = NWT / 4, Q0 = h * GH;  // granules of this wave
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
@@ -584,7 +552,7 @@ void k5_f32s(K5Args32 a) {
             }
         };
         auto body = [&](int64_t tt, int buf, int nbuf, Regs& cx, Regs& nx, bool pf) {
-            float* ts = tsm[slot][DEFER ? (int)(tt & 1) : 0];
+            float* ts = tsm[slot][(int)(tt & 1)];
             const int64_t tb = tbase(tt);
             const int64_t o = (tb >> 2) + lane;
             if (pf) {
@@ -604,26 +572,7 @@ void k5_f32s(K5Args32 a) {
             const float* cR = sC[buf];
             const f4* cL = reinterpret_cast<const f4*>(cR + il * LDC);
             f4 Lv = f4{0.0f, 0.0f, 0.0f, 0.0f};
-            if constexpr (SPLIT) {
-                if constexpr (h == 0) {  // both K halves, each summed as the exchange did
-                    f4 lp[2];
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        f4 lacc[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                        for (int s4 = hh * (KSH / 4); s4 < (hh + 1) * (KSH / 4); ++s4) {
-                            const int gl = tg * (KS / 4) + s4;
-                            const f4 c = cL[gran(gl / G, gl % G)];
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
-                        }
-                        lp[hh] = (lacc[0] + lacc[1]) + (lacc[2] + lacc[3]);
-                    }
-                    Lv = lp[0] + lp[1];
-                }
-            } else {
+            {
                 f4 lacc[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -677,7 +626,7 @@ void k5_f32s(K5Args32 a) {
                 for (int s = 0; s < 4; ++s) tv[s] = ts[il * 17 + 4 * s + tg];
                 T4[o] = tv;
             }
-            if constexpr (DEFER && h == 1) {
+            if constexpr (h == 1) {
                 // W of tile tt-1: its T (written by the partner in step tt-1,
                 // before that step's closing barrier) and its C^ slice
                 if (tt > 0) {
@@ -686,13 +635,7 @@ void k5_f32s(K5Args32 a) {
                     for (int r = 0; r < 4; ++r) tr[r] = tp[(4 * tg + r) * 17 + il];
                     wmfma(sC[(int)((tt + NSL - 1) % NSL)], tr);
                 }
-            } else if constexpr (!SPLIT) {
-                if (K5F_LEAN && !DEFER) {
-                    __syncthreads();  // T of this tile in ts (h = 0 wrote it above)
-                    if (h == 1)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) tr[r] = ts[(4 * tg + r) * 17 + il];
-                }
+            } else {
                 wmfma(cR, tr);
             }
             if (pf) stage_store(nbuf);
@@ -711,7 +654,7 @@ void k5_f32s(K5Args32 a) {
         stage_store(0);
         __syncthreads();
         int64_t tt = 0;
-        if constexpr (DEFER) {
+        {
             // slices rotate over three buffers: tile tt in tt % 3
             int b0 = 0;
             for (; tt + 2 < ntt; tt += 2) {
@@ -734,17 +677,6 @@ void k5_f32s(K5Args32 a) {
                 for (int r = 0; r < 4; ++r) tr[r] = tp[(4 * tg + r) * 17 + il];
                 wmfma(sC[(int)((ntt - 1) % NSL)], tr);
             }
-        } else {
-            for (; tt + 2 < ntt; tt += 2) {
-                body(tt, 0, 1, xa, xb, true);
-                body(tt + 1, 1, 0, xb, xa, true);
-            }
-            if (tt + 1 < ntt) {
-                body(tt, 0, 1, xa, xb, true);
-                body(tt + 1, 1, 0, xb, xa, false);
-            } else {
-                body(tt, 0, 1, xa, xb, false);
-            }
         }
         // W^T C/D layout: M-tile m row rho = 4(l>>4) + rr, col ij = l & 15,
         // k = rho * MT + m; this half's m = 4(h*GH + q) + u
@@ -754,15 +686,15 @@ void k5_f32s(K5Args32 a) {
         for (int mq = 0; mq < NWT; ++mq)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int m = (SPLIT ? 0 : 4 * h * GH) + mq;
+                const int m = 4 * h * GH + mq;
                 const int k = (4 * tg + rr) * MT + m;
                 wl[slot * WS + k * 16 + il] = wacc[mq][rr];
             }
     };
-    // the pair's roles alternate between workgroups (LEAN: the h = 0 wave
-    // carries the elementwise chain; the two workgroups resident on a CU then
-    // put it on different SIMDs, as far as waves map to SIMDs in order)
-    const int hrole = (wid & 1) ^ ((K5F_LEAN > 1) ? (int)(blockIdx.x & 1) : 0);
+    // the pair's roles alternate between workgroups (the h = 0 wave carries
+    // the elementwise chain; the two workgroups resident on a CU then put it
+    // on different SIMDs, as far as waves map to SIMDs in order)
+    const int hrole = (wid & 1) ^ (int)(blockIdx.x & 1);
     if (hrole)
         walk(std::integral_constant<int, 1>{});
     else
@@ -801,11 +733,8 @@ void k5_f32s(K5Args32 a) {
     }
 }
 
-bool k5_split32(const Geom& g) {
-    if (g.RP != 256) return false;
-    const char* e = std::getenv("TRITD_K5F_SPLIT");
-    return !(e && std::atoi(e) == 0);
-}
+// RP = 256 runs the pair kernel (one-wave k5_f32<256>: 16.86 vs 16.30 ms, round 2)
+bool k5_split32(const Geom& g) { return g.RP == 256; }
 int k5_parts32(const Geom& g) { return k5_split32(g) ? (int)cdiv(g.tiles, 2) : k5_grid(g); }
 
 void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st) {

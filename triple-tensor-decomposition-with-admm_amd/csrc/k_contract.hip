@@ -10,6 +10,7 @@
 // F*F.' = (B^TB) o (C^TC) is the Hadamard identity of the Khatri-Rao design
 // matrices built by buildF/G/H (buildF.m:17-21): F, G, H are never formed.
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <cstdlib>
 #include <utility>
@@ -71,70 +72,12 @@ __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__
     }
 }
 
-// The same with 16-byte loads: a lane sums rows 2l, 2l+1 of a 128-row block
-// (8 independent d2v chains), the JS waves split j.
-template <int JS>
-__global__ __launch_bounds__(64 * JS) void k_m1v(const double* __restrict__ Wk,
-                                                 const double* __restrict__ Bh, double* M1,
-                                                 int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                                 const int* stop) {
-    if (*stop) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t i = (int64_t)blockIdx.x * 128 + 2 * lane;
-    const int k = blockIdx.y;
-    d2v acc[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] = d2v{0.0, 0.0};
-    if (i < n1p) {
-        const d2v* wp = reinterpret_cast<const d2v*>(Wk + (int64_t)k * plane + i);
-        const double* bp = Bh + k;
-        const int64_t ld = n1p >> 1;  // d2v per fibre
-        int64_t j = w;
-        for (; j + 7 * JS < n2; j += 8 * JS) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const d2v x = wp[(j + JS * u) * ld];
-                const double b = bp[(j + JS * u) * RP];
-                acc[u][0] = fma(x[0], b, acc[u][0]);
-                acc[u][1] = fma(x[1], b, acc[u][1]);
-            }
-        }
-        for (; j < n2; j += JS) {
-            const d2v x = wp[j * ld];
-            const double b = bp[j * RP];
-            acc[0][0] = fma(x[0], b, acc[0][0]);
-            acc[0][1] = fma(x[1], b, acc[0][1]);
-        }
-    }
-    __shared__ d2v red[JS][64];
-    red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-    __syncthreads();
-    if (w == 0 && i < n1p) {
-        d2v t = red[0][lane];
-#pragma unroll
-        for (int q = 1; q < JS; ++q) t += red[q][lane];
-        M1[i * RP + k] = t[0];
-        M1[(i + 1) * RP + k] = t[1];
-    }
-}
-
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
                hipStream_t st) {
     // 4 slices when the row blocks alone fill the chip (512 rows: 36 vs 39 us
     // with 16), 16 for short shards (64 rows: 64 blocks)
-    const char* v = std::getenv("TRITD_M1V");  // experiment knob
-    const int mv = v ? std::atoi(v) : 0;
-    if (mv) {
-        const dim3 gv((unsigned)cdiv(g.n1p, 128), g.RP);
-        if (mv == 8)
-            hipLaunchKernelGGL(k_m1v<8>, gv, dim3(64 * 8), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
-        else if (mv == 16)
-            hipLaunchKernelGGL(k_m1v<16>, gv, dim3(64 * 16), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
-        else
-            hipLaunchKernelGGL(k_m1v<4>, gv, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop);
-        TRITD_CHECK_LAUNCH();
-        return;
-    }
+    // (16-byte-load variants, two rows per lane, measured neutral or slower
+    // in the solver: DESIGN.md §4)
     const dim3 grid((unsigned)cdiv(g.n1p, 64), g.RP);
     if (g.n1p >= 256)  // (two rows per lane with 16-B loads halves the waves: 72 vs 36 us)
         hipLaunchKernelGGL(k_m1<4>, grid, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
@@ -355,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
                                                   const double* __restrict__ Bh, double* part,
                                                   int64_t n2, int64_t n3p, int64_t ntt,
                                                   int64_t qper, int64_t J, int S,
-                                                  const int* stop, int stagger, SideSolve side) {
+                                                  const int* stop, SideSolve side) {
     if (*stop) return;
     // side job: workgroup 0 runs the R x R solve of update_C (sweep.h)
     if (side.on && blockIdx.x == 0) {
@@ -365,11 +308,6 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
     }
     const int64_t bid = (int64_t)blockIdx.x - side.on;
     WT_BEGIN();
-    // the second workgroup a CU receives starts later, so that the two waves
-    // sharing each SIMD are out of phase (their copy/wait boundaries would
-    // otherwise leave the matrix pipe idle together)
-    if (stagger && bid >= 256)
-        for (int q = 0; q < stagger; ++q) __builtin_amdgcn_s_sleep(64);
     constexpr int MT = RP / 16;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = threadIdx.x & 63;
@@ -426,20 +364,6 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
                 for (int n = 0; n < 4; ++n) acc[m][n] = mfma4(a, c.b[n][s >> 1][s & 1], acc[m][n]);
             }
     };
-#if K2_UNROLL2
-    // two register sets by name: each step computes on the batch issued a
-    // step ago while the next batch lands in the other set
-    Nx xa, xb;
-    if (j0 < j1) load(j0, xa);
-    int64_t j = j0;
-    for (; j + 1 < j1; j += 2) {
-        load(j + 1, xb);
-        mm(xa);
-        if (j + 2 < j1) load(j + 2, xa);
-        mm(xb);
-    }
-    if (j < j1) mm(xa);
-#else
     // one fibre per step: take the batch issued a step ago, issue the next
     Nx cur, nxt;
     if (j0 < j1) load(j0, nxt);
@@ -448,7 +372,6 @@ __global__ __launch_bounds__(256, 2) void k_m3_cp(const double* __restrict__ T,
         if (j + 1 < j1) load(j + 1, nxt);
         mm(cur);
     }
-#endif
 
     // fixed-order sum of the 4 waves: (w2,w3) -> (w0,w1), then w1 -> w0
     constexpr int PER = MT * 16;  // doubles per lane
@@ -524,19 +447,10 @@ __global__ __launch_bounds__(256) void k_m3_reduce(const double* __restrict__ pa
     if (q == 0 && e < count) M3[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-// total waves of one K2 launch (TRITD_M3_WAVES: experiments): about two per SIMD
-static int64_t m3_waves() {  // TRITD_M3_WAVES (experiments); 0: the CP kernel's own choice
-    static const int64_t waves = [] {
-        const char* e = std::getenv("TRITD_M3_WAVES");
-        return e ? (int64_t)std::atoll(e) : (int64_t)0;
-    }();
-    return waves;
-}
-
 // generic kernel: waves per t-block (multiple of 4)
 int m3_split(const Geom& g) {
     const int64_t ntb = cdiv(g.ntt, 4);
-    int64_t S = (m3_waves() > 0 ? m3_waves() : 2048) / ntb;
+    int64_t S = 2048 / ntb;  // about two waves per SIMD
     if (S > g.tiles) S = g.tiles;
     S = (S + 3) / 4 * 4;
     if (S < 4) S = 4;
@@ -559,11 +473,10 @@ static M3Cp m3_cp_split(const Geom& g) {
     // the side solve's workgroup instead of displacing a compute one
     // (shard timings, 64-row shard: K2 + reduce 63.9 -> 55.8 us; 128 rows
     // 97.3 -> 88.0; 256 rows 161 -> 157; 512 rows 2048 waves stay ~1 % ahead)
-    int64_t waves = m3_waves();
-    if (waves <= 0) {
-        const int64_t J2 = 2048 / (ntb * c.qper);
-        waves = (J2 >= 1 && g.n2 / J2 >= 64) ? 2048 : 1024;
-    }
+    // (config 3 with 2 048 / 4 096 waves instead: 0.052 / 0.068 vs 0.048 ms,
+    // profiles/round3/ab_c3_m3_waves.txt)
+    const int64_t J2 = 2048 / (ntb * c.qper);
+    const int64_t waves = (J2 >= 1 && g.n2 / J2 >= 64) ? 2048 : 1024;
     int64_t J = waves / (ntb * c.qper);
     if (J < 1) J = 1;
     if (J > g.n2) J = g.n2;
@@ -572,15 +485,8 @@ static M3Cp m3_cp_split(const Geom& g) {
     return c;
 }
 
-static int m3_stagger() {  // experiment knob: TRITD_M3_STAGGER x 64 x 64 cycles
-    const char* e = std::getenv("TRITD_M3_STAGGER");
-    return e ? std::atoi(e) : 0;
-}
-
-static bool m3_use_cp(int64_t ahj) {
-    static const bool old = std::getenv("TRITD_M3_OLD") != nullptr;  // A/B experiments
-    return ahj == 0 && !old;
-}
+// the CP model's K2 (k_m3_cp); Qi's H rows change with j (k_m3)
+static bool m3_use_cp(int64_t ahj) { return ahj == 0; }
 
 int m3_parts(const Geom& g) {
     const int a = m3_split(g) / 4, b = m3_cp_split(g).S / 4;
@@ -618,7 +524,7 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
             }                                                                                 \
             hipLaunchKernelGGL((k_m3_cp<RPV, LDAV>), dim3(grid.x + side.on), dim3(256), lds, st, T, \
                                Ah + (KOFF), Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, \
-                               cs.J, S, stop, m3_stagger(), side);                   \
+                               cs.J, S, stop, side);                                 \
         } else {                                                                              \
             hipLaunchKernelGGL((k_m3<RPV, LDAV>), grid, dim3(256), lds, st, T, Ah + (KOFF),   \
                                Bh + (KOFF), part + (KOFF), g.n1p, g.n3p, g.ntt, g.tiles, S, stop, ahj, bhj); \
@@ -711,7 +617,8 @@ void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* st
 }
 
 // ---------------------------------------------------------------------------
-// Ginv = inv(P o Q + alpha I), RP/8 wavefronts, matrix in registers.
+// The symmetric Gauss-Jordan sweep (sweep.h: sweep_all; the R x R solves
+// inside M2/K2/K5 and the fallback of k_solve_ns below).
 // The R x R matrix is embedded in RP x RP with an identity pad.  It is SPD
 // (ridge alpha > 0), so Gauss-Jordan needs no pivoting, and its symmetric
 // form (the sweep operator) keeps the matrix symmetric at every step, so
@@ -731,50 +638,6 @@ void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* st
 // no divergent branch and no per-element runtime mask inside or after the
 // sweep (either made the compiler keep every step's values and spill).
 // ---------------------------------------------------------------------------
-#ifndef SOLVE_ROWS_OVERRIDE
-constexpr int SOLVE_ROWS = 8;  // matrix rows per lane; RP/8 waves
-#else
-constexpr int SOLVE_ROWS = SOLVE_ROWS_OVERRIDE;  // tools/solve_bench.hip
-#endif
-
-template <int RP>
-__global__ __launch_bounds__(RP * 64 / SOLVE_ROWS) void k_solve(const double* __restrict__ P,
-                                                               const double* __restrict__ Q,
-                                                               int R, double alpha, double* Ginv,
-                                                               int* flags, const int* stop) {
-    if (*stop) return;
-    // runs beside the big kernels (side stream): win instruction issue on
-    // the shared SIMDs, it is on the critical path of the next apply
-    __builtin_amdgcn_s_setprio(3);
-    constexpr int RW = SOLVE_ROWS, NW = RP / RW, NT = NW * 64;
-    __shared__ double rowbuf[2 * NW * 64];
-    __shared__ double pivs[RP];
-    __shared__ double outb[RP * 64];
-    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int cc = c < RP ? c : 0;  // lanes >= RP read a valid column, never written back
-    double a[RW];
-#pragma unroll
-    for (int q = 0; q < RW; ++q) {
-        const int i = RW * w + q;
-        const bool in = (i < R) && (c < R);
-        const double pq = P[i * RP + cc] * Q[i * RP + cc];
-        const double g = (i == c) ? pq + alpha : pq;
-        a[q] = in ? g : ((i == c) ? 1.0 : 0.0);
-    }
-    rowbuf[w * 64 + c] = a[0];  // row 0 (wave 0's)
-    __syncthreads();
-    sweep_all<RP, RW>(a, rowbuf, pivs, c, w, std::make_integer_sequence<int, RP>{});
-    // out through LDS, then a linear copy that zeroes the pad (the sweep
-    // leaves the identity-pad block and the zero blocks beside it untouched)
-#pragma unroll
-    for (int q = 0; q < RW; ++q) outb[(RW * w + q) * 64 + c] = -a[q];
-    __syncthreads();
-    for (int e = threadIdx.x; e < RP * RP; e += NT) {
-        const int i = e / RP, j = e - (e / RP) * RP;
-        Ginv[e] = (i < R && j < R) ? outb[i * 64 + j] : 0.0;
-    }
-    pinv_request<NT>(pivots_near_cutoff(pivs, R), P, Q, R, RP, alpha, Ginv);
-}
 
 
 // ---------------------------------------------------------------------------
@@ -955,19 +818,10 @@ __global__ __launch_bounds__(RP * 16) void k_solve_ns(const double* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Ginv = inv(P o Q + alpha I) for RP in {128, 256} (fp32 path, r = 9..16):
-// blocked symmetric sweep, one 1024-thread workgroup.  The RP x RP matrix S
-// lives in Ginv (global, L2-resident); thread t owns column c = t % RP and
-// the ROWS = RP*RP/1024 rows of strip t / RP, and only ever touches its own
-// entries there (no cross-thread global traffic, so no L1 coherence
-// question); rows are shared through LDS.  Per block K of 16 pivots:
-//   panel <- S_K (rows K, all columns)                         (LDS)
-//   M = inv(S_KK): one wave sweeps the 16 x 16 block in registers (its
-//       pivots are the sequential sweep's pivots -> pinv-tolerance check)
-//   X = M S_K                                                  (LDS)
-//   S_ij -= sum_k S_ik X_kj (i, j outside K); S_Kj = X_Kj; S_iK = X_Ki;
-//   S_KK = -M            (= sweeping the 16 pivots one by one, blocked)
-// After all blocks S = -inv: Ginv = -S, identity pad zeroed.
+// Register sweep of one 16 x 16 diagonal block (k_solve_mw's owner step):
+// lane c holds column c (the 4 lane groups of the wave sweep identical
+// copies), pivot rows shared through LDS; the pivots are recorded for the
+// pinv-tolerance check.
 // ---------------------------------------------------------------------------
 constexpr int SB = 16;  // pivots per block (a 32-wide register sweep does not fit the 128 VGPRs of a 1024-thread block)
 
@@ -996,112 +850,13 @@ __device__ __forceinline__ void sweep32_all(double (&a)[SB], double* rowp, doubl
     (sweep32_step<Ps>(a, rowp, pv, c), ...);
 }
 
-template <int RP>
-__global__ __launch_bounds__(1024) void k_solve_big(const double* __restrict__ P,
-                                                    const double* __restrict__ Q, int R,
-                                                    double alpha, double* S, int* flags,
-                                                    const int* stop) {
-    if (*stop) return;
-    constexpr int ROWS = RP * RP / 1024;
-    extern __shared__ double sh[];
-    double* panel = sh;              // [SB][RP]
-    double* X = panel + SB * RP;     // [SB][RP]
-    double* M = X + SB * RP;         // [SB][SB]
-    double* rowp = M + SB * SB;      // [64]
-    double* pivs = rowp + 64;        // [RP]
-    const int tid = threadIdx.x;
-    const int c = tid % RP, rb = tid / RP;
-    const int r0 = rb * ROWS;
-    // S = P o Q + alpha I in the leading R x R block, identity pad
-#pragma unroll 1
-    for (int q = 0; q < ROWS; ++q) {
-        const int i = r0 + q;
-        double v;
-        if (i < R && c < R) {
-            v = P[i * RP + c] * Q[i * RP + c];
-            if (i == c) v = v + alpha;
-        } else {
-            v = (i == c) ? 1.0 : 0.0;
-        }
-        S[i * RP + c] = v;
-    }
-    for (int k0 = 0; k0 < RP; k0 += SB) {
-        // panel <- rows K (each owner writes its own entries)
-    #pragma unroll 1
-    for (int q = 0; q < ROWS; ++q) {
-            const int i = r0 + q;
-            if (i >= k0 && i < k0 + SB) panel[(i - k0) * RP + c] = S[i * RP + c];
-        }
-        __syncthreads();
-        // M = inv(S_KK) by a register sweep of the 16 x 16 block in wave 0
-        // (a wave-uniform test: under a divergent one the sweep spills; the 4
-        // lane groups of the wave sweep identical copies)
-        if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
-            const int cc = tid & (SB - 1);
-            double a[SB];
-#pragma unroll
-            for (int i = 0; i < SB; ++i) a[i] = panel[i * RP + k0 + cc];
-            sweep32_all(a, rowp, pivs + k0, cc, std::make_integer_sequence<int, SB>{});
-#pragma unroll
-            for (int i = 0; i < SB; ++i) M[i * SB + cc] = -a[i];
-        }
-        __syncthreads();
-#pragma unroll 1
-        for (int e = tid; e < SB * RP; e += 1024) {  // X = M S_K
-            const int k = e / RP, jj = e - k * RP;
-            double x = 0.0;
-#pragma unroll 8
-            for (int l = 0; l < SB; ++l) x = fma(M[k * SB + l], panel[l * RP + jj], x);
-            X[e] = x;
-        }
-        __syncthreads();
-        const bool cK = c >= k0 && c < k0 + SB;
-        double xc[SB];  // this thread's column of X, reused by all its rows
-#pragma unroll
-        for (int k = 0; k < SB; ++k) xc[k] = X[k * RP + c];
-        // rows in chunks of 8: their L2 loads are in flight together
-#pragma unroll 1
-        for (int q0 = 0; q0 < ROWS; q0 += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = S[(r0 + q0 + u) * RP + c];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = r0 + q0 + u;
-                const bool iK = i >= k0 && i < k0 + SB;
-                double w = v[u];
-#pragma unroll
-                for (int k = 0; k < SB; ++k) w = w - panel[k * RP + i] * xc[k];
-                if (iK && cK)
-                    w = -M[(i - k0) * SB + (c - k0)];
-                else if (iK)
-                    w = X[(i - k0) * RP + c];
-                else if (cK)
-                    w = X[(c - k0) * RP + i];
-                S[i * RP + c] = w;
-            }
-        }
-        __syncthreads();
-    }
-    // Ginv = -S, pad zeroed (each thread its own entries)
-#pragma unroll 1
-    for (int q = 0; q < ROWS; ++q) {
-        const int i = r0 + q;
-        S[i * RP + c] = (i < R && c < R) ? -S[i * RP + c] : 0.0;
-    }
-    pinv_request<1024>(pivots_near_cutoff(pivs, R), P, Q, R, RP, alpha, S);
-}
-
-static size_t solve_big_lds(int RP) {
-    return (size_t)(2 * SB * RP + SB * SB + 64 + RP) * sizeof(double);
-}
 
 // ---------------------------------------------------------------------------
 // Ginv = inv(P o Q + alpha I) at RP = 128 / 256 across NB = RP/16 workgroups
-// (k_solve_mw): the blocked symmetric sweep of k_solve_big, with S split
-// into row strips.  k_solve_big keeps S in one workgroup and moves all of it
-// through that CU's LDS/L2 port on every block step (0.75 ms at RP = 256,
-// on the critical path of config 5's update_B, triple_decomp_ADMM.m:86).
+// (k_solve_mw): a blocked symmetric sweep with S split into row strips.  (A
+// one-workgroup form that kept S in one CU moved all of it through that CU's
+// LDS/L2 port on every block step: 0.75 ms at RP = 256, on the critical path
+// of config 5's update_B, triple_decomp_ADMM.m:86; this form 0.15 ms.)
 // Here workgroup b owns rows [16b, 16b+16) in its LDS (32 KB at 256) and
 // block step K is:
 //   owner (b = K): M = inv(S_KK) (one wave, register sweep: the sequential
@@ -1110,8 +865,8 @@ static size_t solve_big_lds(int RP) {
 //     (global scratch of its Ginv buffer) and then step word K = epoch;
 //   others: wait for step word K, then S_I,j -= S_IK X_Kj (f64 MFMA, the old
 //     S_IK from registers) and S_IK <- (X_K,I)^T.
-// The arithmetic is k_solve_big's (same blocks, same order per block), so
-// the accuracy is too.  Cross-workgroup order: the owner's stores, an agent-
+// The arithmetic per block is the sequential sweep's blocked form (same
+// blocks, same order per block as the one-workgroup kernel it replaced).  Cross-workgroup order: the owner's stores, an agent-
 // scope release fence, a barrier and a release store of the step word; the
 // waiter's acquire load of it, a barrier and an agent-scope acquire fence in
 // every thread.  Only workgroup 0 reads the stop flag; a stopped launch
@@ -1127,13 +882,21 @@ static size_t solve_big_lds(int RP) {
 constexpr int MW_NT = 256;  // 4 waves per workgroup
 constexpr unsigned MW_STOP = 0x80000000u;
 
-__device__ __forceinline__ unsigned mw_wait(const unsigned* w, unsigned epoch, int* flags) {
+// Safety net, not a schedule: the workgroups of a launch depend only on
+// earlier steps, so a slow peer (late dispatch, preemption) only delays the
+// chain.  A wait of ~1 s of polls gives up instead of hanging the device: it
+// raises flags bit 2 (sync() turns it into an error) and the solver's stop
+// flag, so every later kernel of the enqueued iterations skips its work
+// rather than running on a half-swept inverse.
+__device__ __forceinline__ unsigned mw_wait(const unsigned* w, unsigned epoch, int* flags,
+                                            const int* stop) {
     unsigned v = 0;
     for (int n = 0;; ++n) {
         v = __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if ((v & ~MW_STOP) == epoch) return v;
-        if (n > (1 << 22)) {  // ~1 s of polls: give up, never hang the device
+        if (n > (1 << 22)) {
             atomicOr(flags, 2);
+            atomicExch(const_cast<int*>(stop), 1);
             return MW_STOP;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -1184,7 +947,7 @@ __global__ __launch_bounds__(MW_NT) void k_solve_mw(const double* __restrict__ P
         const int k0 = SB * K;
         double* XK = Xg + (int64_t)K * SB * RP;
         if (b == K) {
-            // M = inv(S_KK): wave 0 sweeps the block in registers (k_solve_big's sweep)
+            // M = inv(S_KK): wave 0 sweeps the block in registers (sweep32_all)
             if (w == 0) {
                 const int cc = lane & (SB - 1);
                 double a[SB];
@@ -1222,7 +985,7 @@ __global__ __launch_bounds__(MW_NT) void k_solve_mw(const double* __restrict__ P
             __syncthreads();
             if (tid == 0) __hip_atomic_store(&sync[K], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            if (tid == 0) state = mw_wait(&sync[K], epoch, flags);
+            if (tid == 0) state = mw_wait(&sync[K], epoch, flags, stop);
             // old S_IK as the A operands (A[m][k] = -S(i0+m, k0+4s+k)) before any write
             double a[SB / 4];
 #pragma unroll
@@ -1265,256 +1028,46 @@ __global__ __launch_bounds__(MW_NT) void k_solve_mw(const double* __restrict__ P
     }
 }
 
+// Process-wide epoch counter.  Sessions may be driven from several host
+// threads (ctypes releases the GIL; a device group runs one thread per
+// device), so the increment is atomic: every launch gets an epoch no other
+// launch has had for 2^31 launches, and each Ginv buffer's step words
+// therefore never see the same epoch twice in a row.
+static std::atomic<unsigned> g_mw_epoch{0};
 static unsigned mw_epoch() {
-    static unsigned e = 0;
-    e = (e + 1) & ~MW_STOP;
-    if (e == 0) e = 1;
-    return e;
-}
-
-// ---------------------------------------------------------------------------
-// Ginv = inv(P o Q + alpha I) at RP = 128 (fp32 path, r = 9..11): blocked
-// symmetric sweep with the matrix S in LDS (153 KB).  Per block K of 16
-// pivots (k0 = 16K):
-//   1. wave 0 sweeps the 16-row panel S_K,: pivot by pivot in registers
-//      (lane = column, pivot column by readlane) and records each pivot row
-//      at its pivot divided by the pivot, u_p = S_p,:/d_p; the pivots are the
-//      sequential sweep's (= LDL^T) pivots, kept for the pinv-tolerance check
-//   2. S_ij -= sum_p l_p[i] u_p[j] for i, j outside K (rank-16 f64 MFMA),
-//      with l_p[i] = u_p[i] d_p standing in for the column value S_ip, and
-//      S_iK = S_Kiᵀ
-// Accuracy (80-bit reference, 100-iteration solve of the sensor shape whose
-// Gram reaches cond ~1e6): the sequential sweep lands within 6e-11; this
-// form, whose column values come from the mirrored panel row, within
-// 3e-8..2e-7 — far below single precision, but not enough for the fp64
-// tolerance, so RP <= 64 uses the per-pivot sweep (k_solve).  (Forming D^-1
-// explicitly and multiplying, the textbook blocked form: 3e-5.)  Every
-// variant keeps RP sequential pivot steps of ~0.3 us (broadcast, IEEE
-// division, dependent update), so blocking pays only where the trailing
-// work dominates: 100 us vs 143 us for k_solve_big at RP = 128.
-// After all blocks S = -inv(.): Ginv = -S, identity pad zeroed.
-// ---------------------------------------------------------------------------
-template <int RP>
-constexpr int solve_blk_waves() { return RP >= 128 ? 8 : 4; }
-constexpr size_t solve_blk_lds(int RP) {
-    return ((size_t)RP * (RP + 4) + (size_t)16 * RP + RP) * sizeof(double);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const int2 b = __builtin_bit_cast(int2, v);
-    int2 r;
-    r.x = __builtin_amdgcn_readlane(b.x, l);
-    r.y = __builtin_amdgcn_readlane(b.y, l);
-    return __builtin_bit_cast(double, r);
-}
-
-template <int RP>
-__global__ __launch_bounds__(64 * solve_blk_waves<RP>()) void k_solve_blk(
-    const double* __restrict__ P, const double* __restrict__ Q, int R, double alpha, double* Ginv,
-    int* flags, const int* stop) {
-    if (*stop) return;
-    __builtin_amdgcn_s_setprio(3);  // beside K5 / M3 on the side stream: win issue
-    constexpr int LD = RP + 4, NB = RP / 16, NWV = solve_blk_waves<RP>(), NT = 64 * NWV;
-    constexpr int CPL = (RP + 63) / 64;  // panel columns per lane
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* S = sm;
-    double* Ub = sm + RP * LD;  // [16][RP]: u_p = S_p,: / d_p at pivot p
-    double* pivs = Ub + 16 * RP;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int m = lane & 15, kq = lane >> 4;
-    {
-        constexpr int NE = (RP * RP + NT - 1) / NT;
-        double v[NE];
-#pragma unroll
-        for (int q = 0; q < NE; ++q) {  // loads first
-            const int e = tid + q * NT;
-            const int i = e / RP, c = e - (e / RP) * RP;
-            const bool in = e < RP * RP && i < R && c < R;
-            v[q] = in ? P[e] * Q[e] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < NE; ++q) {
-            const int e = tid + q * NT;
-            const int i = e / RP, c = e - (e / RP) * RP;
-            if (e < RP * RP) S[i * LD + c] = (i == c) ? ((i < R) ? v[q] + alpha : 1.0) : v[q];
-        }
+    for (;;) {
+        const unsigned e = (g_mw_epoch.fetch_add(1, std::memory_order_relaxed) + 1) & ~MW_STOP;
+        if (e != 0) return e;
     }
-    __syncthreads();
-    for (int K = 0; K < NB; ++K) {
-        const int k0 = 16 * K;
-        if (w == 0) {
-            double pv[CPL][16];
-#pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                const int c = lane + 64 * u;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) pv[u][r] = c < RP ? S[(k0 + r) * LD + c] : 0.0;
-            }
-            const int pl0 = k0 & 63, pu = k0 >> 6;  // lane / register set of pivot column k0
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                double colp[16];  // S_rp, r in K (current), from the lane owning column p
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    double x = pv[0][r];
-#pragma unroll
-                    for (int u = 1; u < CPL; ++u) x = (pu == u) ? pv[u][r] : x;
-                    colp[r] = readlane_f64(x, pl0 + q);
-                }
-                const double d = colp[q];
-                const double inv = 1.0 / d;
-#pragma unroll
-                for (int u = 0; u < CPL; ++u) {
-                    const int c = lane + 64 * u;
-                    const bool cp = (c == k0 + q);
-                    const double sc = pv[u][q] * inv;  // a_pc / d
-                    if (c < RP) Ub[q * RP + c] = sc;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const double sw = pv[u][r] - colp[r] * sc;
-                        const double cq = colp[r] * inv;
-                        pv[u][r] = (r == q) ? (cp ? -inv : sc) : (cp ? cq : sw);
-                    }
-                }
-                if (lane == 0) pivs[k0 + q] = d;
-            }
-#pragma unroll
-            for (int u = 0; u < CPL; ++u) {
-                const int c = lane + 64 * u;
-                if (c < RP)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) S[(k0 + r) * LD + c] = pv[u][r];
-            }
-        }
-        __syncthreads();
-        // trailing rank-16 update: A[m][kk] = -l_kk[16it + m], B[kk][n] = u_kk[16jt + n]
-        for (int t = w; t < NB * NB; t += NWV) {
-            const int it = t / NB, jt = t - (t / NB) * NB;
-            if (it == K || jt == K) continue;
-            d4 acc;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] = S[(16 * it + kq + 4 * r) * LD + 16 * jt + m];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const int kk = 4 * s4 + kq;
-                const double l = Ub[kk * RP + 16 * it + m] * pivs[k0 + kk];
-                acc = mfma4(-l, Ub[kk * RP + 16 * jt + m], acc);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) S[(16 * it + kq + 4 * r) * LD + 16 * jt + m] = acc[r];
-        }
-        for (int e = tid; e < 16 * RP; e += NT) {  // column block K (symmetry)
-            const int rr = e / RP, c = e - (e / RP) * RP;
-            if (c < k0 || c >= k0 + 16) S[c * LD + k0 + rr] = S[(k0 + rr) * LD + c];
-        }
-        __syncthreads();
-    }
-    for (int e = tid; e < RP * RP; e += NT) {
-        const int i = e / RP, j = e - (e / RP) * RP;
-        Ginv[e] = (i < R && j < R) ? -S[i * LD + j] : 0.0;
-    }
-    pinv_request<NT>(pivots_near_cutoff(pivs, R), P, Q, R, RP, alpha, Ginv);
-}
-
-template <int RP>
-void launch_solve_blk(int R, const double* P, const double* Q, double alpha, double* Ginv,
-                      int* flags, const int* stop, hipStream_t st) {
-    constexpr size_t lds = solve_blk_lds(RP);
-    static bool attr = false;
-    if (!attr && lds > 65536) {
-        TRITD_HIP(hipFuncSetAttribute((const void*)k_solve_blk<RP>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    }
-    attr = true;
-    hipLaunchKernelGGL(k_solve_blk<RP>, dim3(1), dim3(64 * solve_blk_waves<RP>()), lds, st, P, Q, R,
-                       alpha, Ginv, flags, stop);
 }
 
 // RP <= 64: Newton-Schulz refinement of the previous inverse with the
 // per-pivot sweep as fallback (k_solve_ns); RP = 128 / 256: the multi-
-// workgroup blocked sweep (k_solve_mw).  TRITD_SOLVE=gj runs the plain sweep
-// (k_solve) at RP <= 64, =blk the blocked sweep there (timing / accuracy
-// experiments), =big the one-workgroup kernels at 128 / 256 (k_solve_blk /
-// k_solve_big), =sweep k_solve_big at both.
-static int solve_mode() {
-    static const int v = [] {
-        const char* e = std::getenv("TRITD_SOLVE");
-        if (!e) return 0;
-        const std::string x(e);
-        return x == "blk" ? 1 : (x == "sweep" ? 2 : (x == "gj" ? 3 : (x == "big" ? 4 : 0)));
-    }();
-    return v;
-}
-
+// workgroup blocked sweep (k_solve_mw).
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
                   int* flags, const int* stop, hipStream_t st) {
-#define SOLVE_CASE(RPV)                                                                      \
-    case RPV:                                                                                \
-        hipLaunchKernelGGL(k_solve<RPV>, dim3(1), dim3(RPV * 64 / SOLVE_ROWS), 0, st, P, Q, R, alpha, \
-                           Ginv, flags, stop);                                               \
-        break;
-    if ((RP == 128 || RP == 256) && (solve_mode() == 0 || solve_mode() == 3)) {
-        // multi-workgroup blocked sweep (k_solve_mw): RP/16 workgroups
-        if (RP == 128)
-            hipLaunchKernelGGL(k_solve_mw<128>, dim3(128 / SB), dim3(MW_NT), 0, st, P, Q, R, alpha,
-                               Ginv, flags, stop, mw_epoch());
-        else
-            hipLaunchKernelGGL(k_solve_mw<256>, dim3(256 / SB), dim3(MW_NT), 0, st, P, Q, R, alpha,
-                               Ginv, flags, stop, mw_epoch());
-        TRITD_CHECK_LAUNCH();
-        return;
-    }
-    if ((RP == 128 && solve_mode() != 2) || (RP <= 64 && solve_mode() == 1)) {
-        switch (RP) {
-            case 16: launch_solve_blk<16>(R, P, Q, alpha, Ginv, flags, stop, st); break;
-            case 32: launch_solve_blk<32>(R, P, Q, alpha, Ginv, flags, stop, st); break;
-            case 48: launch_solve_blk<48>(R, P, Q, alpha, Ginv, flags, stop, st); break;
-            case 64: launch_solve_blk<64>(R, P, Q, alpha, Ginv, flags, stop, st); break;
-            case 128: launch_solve_blk<128>(R, P, Q, alpha, Ginv, flags, stop, st); break;
-            default: throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
-        }
-        TRITD_CHECK_LAUNCH();
-        return;
-    }
-    if (RP <= 64 && solve_mode() == 0) {
-        switch (RP) {
+    switch (RP) {
 #define NS_CASE(RPV)                                                                            \
     case RPV:                                                                                   \
         hipLaunchKernelGGL(k_solve_ns<RPV>, dim3(1), dim3(RPV * 16), 0, st, P, Q, R, alpha, Ginv, \
                            flags, stop);                                                        \
         break;
-            NS_CASE(16)
-            NS_CASE(32)
-            NS_CASE(48)
-            NS_CASE(64)
+        NS_CASE(16)
+        NS_CASE(32)
+        NS_CASE(48)
+        NS_CASE(64)
 #undef NS_CASE
-            default: throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
-        }
-        TRITD_CHECK_LAUNCH();
-        return;
-    }
-    switch (RP) {
-        SOLVE_CASE(16)
-        SOLVE_CASE(32)
-        SOLVE_CASE(48)
-        SOLVE_CASE(64)
-        case 128:
-        case 256: {
-            const size_t lds = solve_big_lds(RP);
-            auto kern = RP == 128 ? k_solve_big<128> : k_solve_big<256>;
-            static bool attr[2] = {false, false};
-            if (!attr[RP == 256]) {
-                TRITD_HIP(hipFuncSetAttribute((const void*)kern,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                attr[RP == 256] = true;
-            }
-            hipLaunchKernelGGL(kern, dim3(1), dim3(1024), lds, st, P, Q, R, alpha, Ginv, flags, stop);
+        case 128:  // RP/16 workgroups
+            hipLaunchKernelGGL(k_solve_mw<128>, dim3(128 / SB), dim3(MW_NT), 0, st, P, Q, R, alpha,
+                               Ginv, flags, stop, mw_epoch());
             break;
-        }
+        case 256:
+            hipLaunchKernelGGL(k_solve_mw<256>, dim3(256 / SB), dim3(MW_NT), 0, st, P, Q, R, alpha,
+                               Ginv, flags, stop, mw_epoch());
+            break;
         default:
             throw Error(TRITD_ERR_UNSUPPORTED, "solve: RP not supported");
     }
-#undef SOLVE_CASE
     TRITD_CHECK_LAUNCH();
 }
 

@@ -5,8 +5,6 @@
 // accumulated in single here (W and T are single); the factor operands
 // (A^ o B^, B^, A^) are the double factors rounded to single, as MATLAB
 // converts the double design matrix F/G/H when it meets a single X_k.
-#include <cstdlib>
-
 #include "kernels.h"
 
 namespace tritd {
@@ -20,39 +18,11 @@ __device__ __forceinline__ f4 mfma32c(float a, float b, f4 c) {
 // ---------------------------------------------------------------------------
 // M1(i,k) = sum_j W[k][j*n1p + i] * B^(j,k)   (single)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_m1_32(const float* __restrict__ Wk,
-                                               const double* __restrict__ Bh, float* M1,
-                                               int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                               const int* stop) {
-    if (*stop) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-    const int k = blockIdx.y;
-    float acc[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] = 0.0f;
-    if (i < n1p) {
-        const float* wp = Wk + (int64_t)k * plane + i;
-        const double* bp = Bh + k;
-        int64_t j = w;
-        for (; j + 28 < n2; j += 32) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                acc[u] = fmaf(wp[(j + 4 * u) * n1p], (float)bp[(j + 4 * u) * RP], acc[u]);
-        }
-        for (; j < n2; j += 4) acc[0] = fmaf(wp[j * n1p], (float)bp[j * RP], acc[0]);
-    }
-    __shared__ float red[4][64];
-    red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-    __syncthreads();
-    if (w == 0 && i < n1p) M1[i * RP + k] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-}
-
-// Round 5: 16-byte loads (a lane owns 4 consecutive i, a wave 1 KB of a
-// j-row), U = 8 rows in flight per wave; the 4 waves take every 4th j and are
-// summed through LDS in fixed order.  W at config 5 is 4.3 GB (as big as
-// the tensor) and is read by M1 and M2: the 4-byte kernels above read it at
-// ~4 TB/s (1.06 / 1.24 ms per launch).
+// 16-byte loads (a lane owns 4 consecutive i, a wave 1 KB of a j-row), U = 8
+// rows in flight per wave; the 4 waves take every 4th j and are summed
+// through LDS in fixed order.  W at config 5 is 4.3 GB (as big as the tensor)
+// and is read by M1 and M2: 4-byte-load kernels read it at ~4 TB/s (1.06 /
+// 1.24 ms per launch, round 3).
 __global__ __launch_bounds__(256) void k_m1_32v(const float* __restrict__ Wk,
                                                 const double* __restrict__ Bh, float* M1,
                                                 int64_t n1p, int64_t n2, int64_t plane, int RP,
@@ -102,40 +72,17 @@ __global__ __launch_bounds__(256) void k_m1_32v(const float* __restrict__ Wk,
 
 void launch_m1_32(const Geom& g, const float* Wk, const double* Bh, float* M1, const int* stop,
                   hipStream_t st) {
-    const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;  // A/B: the 4-byte kernels (per launch)
-    if (!old)
-        hipLaunchKernelGGL(k_m1_32v, dim3((unsigned)cdiv(g.n1p, 256), g.RP), dim3(256), 0, st, Wk, Bh,
-                           M1, g.n1p, g.n2, g.plane, g.RP, stop);
-    else
-        hipLaunchKernelGGL(k_m1_32, dim3((unsigned)cdiv(g.n1p, 64), g.RP), dim3(256), 0, st, Wk, Bh,
-                           M1, g.n1p, g.n2, g.plane, g.RP, stop);
+    hipLaunchKernelGGL(k_m1_32v, dim3((unsigned)cdiv(g.n1p, 256), g.RP), dim3(256), 0, st, Wk, Bh,
+                       M1, g.n1p, g.n2, g.plane, g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 
 // ---------------------------------------------------------------------------
 // M2(j,k) = sum_i W[k][j*n1p + i] * A^(i,k)   (single sum, stored as double)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_m2_32(const float* __restrict__ Wk,
-                                               const double* __restrict__ AhT, double* M2,
-                                               int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                               const int* stop) {
-    if (*stop) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t j = blockIdx.x;
-    const int k = blockIdx.y * 4 + w;
-    if (k >= RP) return;
-    const float* wp = Wk + (int64_t)k * plane + j * n1p;
-    const double* ap = AhT + (int64_t)k * n1p;
-    float acc = 0.0f;
-    for (int64_t i = lane; i < n1p; i += 64) acc = fmaf(wp[i], (float)ap[i], acc);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) M2[j * RP + k] = (double)acc;
-}
-
-// Round 5: 16-byte loads, a lane 4 consecutive i per step, four independent
-// accumulators, every load of the row in flight before the sums (n1p/256
-// steps per wave; 8 at config 5).
+// Shards taller than k_m2_32w takes (n1p > 2048): 16-byte loads, a lane 4
+// consecutive i per step, four independent accumulators, every load of the
+// row in flight before the sums.
 __global__ __launch_bounds__(256) void k_m2_32v(const float* __restrict__ Wk,
                                                 const double* __restrict__ AhT, double* M2,
                                                 int64_t n1p, int64_t n2, int64_t plane, int RP,
@@ -236,21 +183,15 @@ __global__ __launch_bounds__(256) void k_m2_32w(const float* __restrict__ Wk,
 
 void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
                   hipStream_t st) {
-    const bool old = std::getenv("TRITD_M1M2_OLD") != nullptr;
-    const char* m2v = std::getenv("TRITD_M2V");  // A/B: 1 = k_m2_32v
     constexpr int UG = 8, JB = 8;
-    if (!old && !(m2v && std::atoi(m2v) == 1) && g.n1p <= 64 * 4 * UG) {
+    if (g.n1p <= 64 * 4 * UG) {
         hipLaunchKernelGGL((k_m2_32w<UG, JB>), dim3((unsigned)cdiv(g.n2, 4 * JB), (unsigned)g.RP),
                            dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
         TRITD_CHECK_LAUNCH();
         return;
     }
-    if (!old)
-        hipLaunchKernelGGL(k_m2_32v, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
-                           AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
-    else
-        hipLaunchKernelGGL(k_m2_32, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
-                           AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
+    hipLaunchKernelGGL(k_m2_32v, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
+                       AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -390,10 +331,9 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
                   double* M3, const int* stop, hipStream_t st) {
     const int64_t jc = m3_jchunks(g), qper = g.n1p >> 4, ntg = cdiv(g.ntt, 4);
     const dim3 grid((unsigned)(ntg * qper * jc)), block(64 * M3W);
-    const bool oldk = std::getenv("TRITD_M3F_OLD") != nullptr;  // A/B (read per launch: tools/ab_env.py)
 #define M3F_CASE(RPV)                                                                              \
     case RPV:                                                                                      \
-        if (RPV >= 64 && !oldk)                                                                    \
+        if (RPV >= 64)                                                                             \
             hipLaunchKernelGGL((k_m3_32<RPV, (RPV >= 64)>), grid, block, 0, st, T, Ah, Bh, part,   \
                                g.n1p, g.n2, g.n3p, g.ntt, jc, stop);                               \
         else                                                                                       \
@@ -419,53 +359,13 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
 }
 
 // ---------------------------------------------------------------------------
-// Y = M * Ginv for any RP (the small-RP path of k_contract.hip stages Ginv in
-// LDS, which stops at RP = 64).  16 rows per block, M rows in LDS, Ginv read
-// from L2 column-wise (coalesced across the block's columns).
-// ---------------------------------------------------------------------------
-template <typename TM>
-__global__ __launch_bounds__(256) void k_apply_gen(const TM* __restrict__ M, int64_t rows,
-                                                   const double* __restrict__ Ginv, int RP,
-                                                   double* Y, double* YT, int64_t ldT, float* YF,
-                                                   int round32, const int* stop) {
-    if (stop && *stop) return;
-    extern __shared__ double msh[];  // 16 x (RP + 1)
-    const int64_t r0 = (int64_t)blockIdx.x * 16;
-    const int LD = RP + 1;
-    for (int e = threadIdx.x; e < 16 * RP; e += 256) {
-        const int rr = e / RP, qq = e - rr * RP;
-        msh[rr * LD + qq] = (r0 + rr < rows) ? (double)M[(r0 + rr) * RP + qq] : 0.0;
-    }
-    __syncthreads();
-    for (int kb = 0; kb < RP; kb += 256) {
-        const int k = kb + (int)threadIdx.x % (RP < 256 ? RP : 256);
-        const int rstep = RP < 256 ? 256 / RP : 1;
-        const int rl = RP < 256 ? (int)threadIdx.x / RP : 0;
-        if (k >= RP) continue;
-        for (int rr = rl; rr < 16; rr += rstep) {
-            const int64_t i = r0 + rr;
-            if (i >= rows) break;
-            double s0 = 0.0, s1 = 0.0;
-            for (int qq = 0; qq < RP; qq += 2) {
-                s0 = fma(msh[rr * LD + qq], Ginv[(int64_t)qq * RP + k], s0);
-                s1 = fma(msh[rr * LD + qq + 1], Ginv[(int64_t)(qq + 1) * RP + k], s1);
-            }
-            double s = s0 + s1;
-            if (round32) s = (double)(float)s;
-            Y[i * RP + k] = s;
-            if (YT) YT[(int64_t)k * ldT + i] = s;
-            if (YF) YF[i * RP + k] = (float)s;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// The same product on f64 MFMA (the default): one wave per 16 x 16 tile of Y,
+// Y = M * Ginv for any RP (fp32 path, fp64 RP > 64) on f64 MFMA: one wave per 16 x 16 tile of Y,
 // A[m][k] = M(r0+m, 4s+k), B[k][n] = Ginv(4s+k, 16ct+n), RP/4 K-steps whose
 // operands are loaded in batches of 16 before their MFMAs (both inputs are
 // L2-resident: M is rows x RP, Ginv RP x RP).  At config 5 (rows 2048,
 // RP 256) k_apply_gen took 0.28 ms per apply, three per iteration on the
-// critical path (128 workgroups of sequential dot products).
+// critical path (128 workgroups of sequential dot products, round 3's
+// k_apply_gen).
 // ---------------------------------------------------------------------------
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -515,8 +415,7 @@ void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, do
                       double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
                       int* flags, hipStream_t st) {
     launch_pinv_fix(RP, Ginv, stop, flags, st);
-    static const bool old = std::getenv("TRITD_APPLY_GEN") != nullptr;  // A/B: the VALU kernel
-    if (!old) {
+    {
         const int64_t tiles = cdiv(rows, 16) * (RP / 16);
         const dim3 grid((unsigned)cdiv(tiles, 4)), block(256);
 #define APPLY_MF_CASE(RPV)                                                                          \
@@ -539,17 +438,7 @@ void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, do
         }
 #undef APPLY_MF_CASE
         TRITD_CHECK_LAUNCH();
-        return;
     }
-    const size_t lds = (size_t)16 * (RP + 1) * sizeof(double);
-    const dim3 grid((unsigned)cdiv(rows, 16)), block(256);
-    if (Mf)
-        hipLaunchKernelGGL(k_apply_gen<float>, grid, block, lds, st, Mf, rows, Ginv, RP, Y, YT, ldT,
-                           YF, (int)round32, stop);
-    else
-        hipLaunchKernelGGL(k_apply_gen<double>, grid, block, lds, st, M, rows, Ginv, RP, Y, YT, ldT,
-                           YF, (int)round32, stop);
-    TRITD_CHECK_LAUNCH();
 }
 
 }  // namespace tritd

@@ -49,13 +49,19 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 // (the caller's column-major array: ldj = n1, ldt = n1*n2; no padded copy).
 // mode 0: write L; mode 1: per-block partials of sum (L-X)^2 and sum X^2
 // (the driver's RRE, traffic_triple_comparison.m:62-63,194-199).
-// A wave owns one ij-tile (16 rows i of one fibre j, KR row in registers);
-// the block stages C^T for TPC t-values at a time in LDS and every wave runs
-// two independent MFMA chains (two t-tiles) per step.  Bound: f64 MFMA
-// (2*N*R flops) for RP >= 32, the N*8 B write below.
+//
+// K5's L half on its own: a wave owns one ij-tile (16 rows i of one fibre j,
+// its Khatri-Rao row in registers) and walks the t-tiles; the workgroup's 4
+// waves share the C^T slice of each t-tile, staged in LDS double-buffered
+// (the slice of t-tile tt+1 is loaded into registers before tile tt's MFMAs
+// and written after them: one barrier per t-tile).  Per t-tile a wave runs
+// RP/4 f64 MFMAs and stores 4 x 128 B pieces of L (16 consecutive i at 4
+// t-values per store).  Bound: f64 MFMA (2*N*R flops); ~70 VGPRs and 17 KB
+// of LDS per workgroup leave several waves per SIMD to cover the stores and
+// the staging.  (Round 3's form staged 32 t-values per step without double
+// buffering, two barriers each: 0.464 ms at 512^3 r = 8, 0.47 of the MFMA peak.)
 // ---------------------------------------------------------------------------
-constexpr int TP_WAVES = 8;
-constexpr int TPC = 32;  // t-values per LDS chunk (two t-tiles)
+constexpr int TP_WAVES = 4;
 
 template <int RP, int MODE>
 __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__ Ah,
@@ -66,8 +72,11 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
                                                       int64_t n3p, int64_t tiles, int64_t ldj,
                                                       int64_t ldt, int64_t ahj, int64_t bhj) {
     constexpr int KS = RP / 4;
-    constexpr int LDT = TPC + 16;  // 2*LDT = 96 = 32 mod 64 dwords: no bank conflicts per half-wave
-    __shared__ double cs[RP * LDT];
+    constexpr int SK = 17;  // odd row stride of the [k][t] slice (K5's L operand layout)
+    constexpr int NT = 64 * TP_WAVES;
+    constexpr int SP = RP * 8;  // d2v pairs per slice (RP rows of 16 t)
+    constexpr int NS = (SP + NT - 1) / NT;
+    __shared__ double sct[2][RP * SK];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int il = lane & 15, tg = lane >> 4;
     const int64_t tile = (int64_t)blockIdx.x * TP_WAVES + wid;
@@ -82,40 +91,60 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
         const int k = 4 * s + tg;
         kr[s] = active ? Ah[j * ahj + i * RP + k] * Bh[j * bhj + k] : 0.0;  // kernels.h: KR source
     }
-    const int64_t obase = i + ldj * j;
-    double sn = 0.0, sd = 0.0;
-    for (int64_t c0 = 0; c0 < n3p; c0 += TPC) {
-        __syncthreads();  // the previous chunk is consumed
-        for (int e = threadIdx.x; e < RP * TPC; e += 64 * TP_WAVES) {
-            const int k = e / TPC, t = e % TPC;
-            cs[k * LDT + t] = (c0 + t < n3p) ? ChT[(int64_t)k * n3p + c0 + t] : 0.0;
-        }
-        __syncthreads();
-        d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    const int64_t ntt = n3p >> 4;
+    d2v sv[NS];
+    auto stage_load = [&](int64_t tt) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const double* row = cs + (4 * s + tg) * LDT + il;
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[0], kr[s], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16], kr[s], acc1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const d4 acc = h ? acc1 : acc0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t t = c0 + 16 * h + tg + 4 * r;
-                if (!row_ok || t >= n3) continue;
-                const int64_t off = obase + ldt * t;
-                if (MODE == 0) {
-                    L[off] = acc[r];
-                } else {
-                    const double x = X[off];
-                    const double dlt = acc[r] - x;
-                    sn += dlt * dlt;
-                    sd += x * x;
-                }
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * NT;
+            if (SP % NT == 0 || e < SP) {
+                const int k = e >> 3, t = (e & 7) * 2;
+                sv[q] = *reinterpret_cast<const d2v*>(ChT + (int64_t)k * n3p + tt * 16 + t);
             }
         }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * NT;
+            if (SP % NT == 0 || e < SP) {
+                const int k = e >> 3, t = (e & 7) * 2;
+                sct[buf][k * SK + t] = sv[q][0];
+                sct[buf][k * SK + t + 1] = sv[q][1];
+            }
+        }
+    };
+    const int64_t obase = i + ldj * j;
+    double sn = 0.0, sd = 0.0;
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    for (int64_t tt = 0; tt < ntt; ++tt) {
+        const int buf = (int)(tt & 1);
+        const bool more = tt + 1 < ntt;
+        if (more) stage_load(tt + 1);
+        const double* cT = sct[buf];
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
+        // C/D element r of lane l: L(i, j, t = 16 tt + (l>>4) + 4r)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t t = tt * 16 + tg + 4 * r;
+            if (!row_ok || t >= n3) continue;
+            const int64_t off = obase + ldt * t;
+            if (MODE == 0) {
+                __builtin_nontemporal_store(acc[r], L + off);
+            } else {
+                const double x = X[off];
+                const double dlt = acc[r] - x;
+                sn = fma(dlt, dlt, sn);
+                sd = fma(x, x, sd);
+            }
+        }
+        if (more) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
+        __syncthreads();
     }
     if (MODE == 1) {
 #pragma unroll
@@ -147,6 +176,7 @@ void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* 
                const double* X, double* partial, int mode, int64_t ldj, int64_t ldt,
                hipStream_t st, int64_t ahj, int64_t bhj) {
     if (bhj < 0) bhj = g.RP;
+    if (g.n3p % 16) throw Error(TRITD_ERR_ARG, "triple_product: n3p must be a multiple of 16");
     const dim3 grid(tp_grid(g)), block(64 * TP_WAVES);
 #define TP_CASE(RPV)                                                                            \
     case RPV:                                                                                   \
@@ -357,8 +387,8 @@ __device__ __forceinline__ double st1(double x, double lam) {
 // for one load per grid-stride step).  Round 5: on zeros four loads per thread
 // timed 0.332 vs 0.337 ms (tools/st_probe.hip; sixteen 0.358, an XCD-major or
 // 1 MB-strided block order 0.36-0.37), but on random data, interleaved in one
-// process (tools/ab_st.py), eight win: 0.3415 vs 0.3459 ms = 6.29 TB/s, the
-// copy ceiling.  TRITD_ST_U=4 keeps the other for A/B.
+// process (tools/ab_st.py at commit eceb414, when ST_U was a knob), eight
+// win: 0.3415 vs 0.3459 ms = 6.29 TB/s, the copy ceiling.
 template <int ST_U>
 __global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict__ X, int64_t n,
                                                         double lam, double* __restrict__ Y) {
@@ -387,15 +417,11 @@ __global__ __launch_bounds__(256) void k_soft_threshold(const double* __restrict
 
 void launch_soft_threshold(const double* X, int64_t n, double lam, double* Y, hipStream_t st) {
     if (((uintptr_t)X | (uintptr_t)Y) & 15) throw Error(TRITD_ERR_ARG, "soft_threshold: 16-B alignment");
-    const char* ue = std::getenv("TRITD_ST_U");  // A/B (read per launch)
-    const int u = ue ? std::atoi(ue) : 8;
-    int64_t blocks = cdiv(n / 2, 256 * (u == 4 ? 4 : 8));
+    constexpr int U = 8;
+    int64_t blocks = cdiv(n / 2, 256 * U);
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
-    if (u == 4)
-        hipLaunchKernelGGL(k_soft_threshold<4>, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
-    else
-        hipLaunchKernelGGL(k_soft_threshold<8>, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
+    hipLaunchKernelGGL(k_soft_threshold<U>, dim3((unsigned)blocks), dim3(256), 0, st, X, n, lam, Y);
     TRITD_CHECK_LAUNCH();
 }
 

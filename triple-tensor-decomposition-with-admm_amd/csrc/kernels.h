@@ -33,7 +33,6 @@ struct K5Args {
     double* E;   // dense E: only tiles whose compact slot overflowed (common.h)
     double* CE;  // compact E: one 32-double slot per tile
     double* YL;
-    double* YO;
     double* T;
     double* Wk;
     const double* Ah;
@@ -45,7 +44,6 @@ struct K5Args {
     IterScalars s;
     const int* stop;
     unsigned long long* dense_tiles;  // DENSE_SLOTS running counts of E tiles stored densely
-    int rot;  // rotate each workgroup's t-walk (0 = natural order)
     // derived-Y_O mode (dy): Y_O is not stored; K5 of iteration k+1 rebuilds
     // Y_O^(k) = Y_L^(k) - muO_k (E^(k) - E^(k-1)) from E^(k) (CE/E) and
     // E^(k-1) (CEp/Ep) and writes E^(k+1) over E^(k-1) (k_admm.hip)
@@ -64,11 +62,11 @@ int k5_grid(const Geom& g);
 int k5_tsplit(const Geom& g);
 int k5_parts32(const Geom& g);  // fp32 K5's norm-partial count (its workgroups)
 // dense_e: E kept densely for every tile (no compact slots; dy only, RP <= 64)
-void launch_k5(const Geom& g, const K5Args& a, bool prologue, bool dy, hipStream_t st,
+void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st,
                bool dense_e = false);
 // O_k = (D + invL_next*Y_L) - T_{k+1} (O is not stored by K5)
-void launch_pool_probe(const Geom& g, double* D, double* YL, double* YO, double* T, double* CE,
-                       bool dy, hipStream_t st);
+void launch_pool_probe(const Geom& g, double* D, double* YL, double* T, double* CE,
+                       hipStream_t st);
 void launch_ce_expand(const Geom& g, const double* CE, double* E, hipStream_t st);
 void launch_o_fixup(const Geom& g, const double* D, const double* YL, const double* T,
                     double invL_next, double* O, hipStream_t st);

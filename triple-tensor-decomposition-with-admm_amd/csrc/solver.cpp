@@ -88,25 +88,20 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
     // K5 / K2 instantiations; fp64 RP = 128/256 runs K5 at one wave per SIMD
     // and K2 as 64-column passes — functional, not the tuned r <= 8 path)
     if (f32_ || g_.R > 64) g_.RP = padded_rank32(g_.R);
+    // K5's t-split is fixed here: W's partial sets, K5's norm partials and
+    // red1_'s tail are all sized by it (fp64 K5 only)
+    if (!f32_) g_.tsplit = k5_tsplit(g_);
+    // Schedules: one GPU without a group stream runs the
+    // single-stream fused iteration (fp64 CP, RP <= 64) or else the
+    // overlapped one (side-stream Grams and solves); with a communicator the
+    // fused iteration with its two all-reduces, or the sharded side-stream
+    // one; device groups sharing a stream run the phase-serial order.
     overlap_ = (comm == nullptr) && (shared_stream == nullptr);
+    dy_ = !f32_;  // derived Y_O (k_admm.hip): every fp64 session
     {
-        const char* ov = std::getenv("TRITD_OVERLAP");
-        ovmode_ = ov ? std::atoi(ov) : 3;
-        const char* rt = std::getenv("TRITD_ROT");
-        rot_ = rt ? std::atoi(rt) : 0;
-        if (ovmode_ == 0) overlap_ = false;
-        // one process per GPU with a communicator: the sharded schedule with
-        // its off-critical-path Grams and solves on the side stream
-        const char* dy = std::getenv("TRITD_DY");
-        dy_ = !f32_ && !(dy && std::atoi(dy) == 0);
-        const char* gm = std::getenv("TRITD_GRAM_MAIN");      // overlapped (1-GPU) schedule
-        gram_main_ = gm ? std::atoi(gm) : 0;
-        const char* sbm = std::getenv("TRITD_SB_MAIN");
-        sb_main_ = !(sbm && std::atoi(sbm) == 0);
-        const char* gms = std::getenv("TRITD_GRAM_MAIN_SH");  // sharded schedule
-        gram_main_sh_ = gms ? std::atoi(gms) : 0;
-        const char* de = std::getenv("TRITD_DENSE_E");
+        const char* de = std::getenv("TRITD_DENSE_E");  // force the E storage form (tests)
         de_mode_ = de ? std::atoi(de) : -1;
+        // TRITD_SHOV=0: a communicator session runs the phase-serial order
         const char* sh = std::getenv("TRITD_SHOV");
         shov_ = comm != nullptr && comm->active() && shared_stream == nullptr &&
                 !(sh && std::atoi(sh) == 0);
@@ -131,8 +126,6 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         // tools/sync_bench.hip); TRITD_FUSED=0 keeps the side-stream schedules
         const char* fe = std::getenv("TRITD_FUSED");
         fused_ = (overlap_ || shov_) && !qi_ && !f32_ && g_.RP <= 64 && !(fe && std::atoi(fe) == 0);
-        const char* ks = std::getenv("TRITD_K2SIDE");
-        k2side_ = ks ? std::atoi(ks) : 1;
     }
 
     // deterministic mu schedule (:16-17, :56-57); muL == muO at every k
@@ -151,8 +144,9 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         // the six streamed tensors live in one pool; each base is staggered so
         // that equal offsets of concurrently streamed tensors do not map to
         // the same HBM channel
-        const char* sg = std::getenv("TRITD_STAGGER");
-        const size_t stagger = sg ? (size_t)std::atoll(sg) : 256;  // measured: tools/stagger_sweep.py
+        // 256 B: measured best of 0..4096 (tools/stagger_sweep.py at commit
+        // 4a7facc, when the stagger was a knob)
+        constexpr size_t stagger = 256;
         const size_t slot = round_up((int64_t)(Np * es_ + 5 * stagger), 4096);
         const size_t pool_bytes = 6 * slot;
         // compact E: 256 B per tile in either data type (before probing: the probe streams it)
@@ -172,7 +166,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         }
     }
     // W, plus the partial sets of a t-split K5 walk (k5_tsplit; fp64)
-    Wk_.alloc_bytes((size_t)g_.RP * g_.plane * es_ * (f32_ ? 1 : (size_t)k5_tsplit(g_)));
+    Wk_.alloc_bytes((size_t)g_.RP * g_.plane * es_ * (size_t)g_.tsplit);
     TRITD_HIP(hipMemsetAsync(Wk_.p, 0, Wk_.bytes(), st_));
     if (f32_) ChF_.alloc_bytes((size_t)g_.n3p * g_.RP * sizeof(float));
     for (int q = 0; q < 2; ++q) {
@@ -459,8 +453,9 @@ void Session::launch_k5_any(int k, bool prologue) {
         return;
     }
     K5Args a{};
-    a.D = D_.p; a.O = O_.p; a.YL = YL_.p; a.YO = YO_.p; a.T = T_.p; a.Wk = Wk_.p;
-    // E^(k-1) is read, E^(k) written (dy: over E^(k-2); otherwise in place)
+    a.D = D_.p; a.O = O_.p; a.YL = YL_.p; a.T = T_.p; a.Wk = Wk_.p;
+    // E^(k-1) and E^(k-2) are read (Y_O is derived from them), E^(k) is
+    // written over E^(k-2)
     a.E = e_buf(k - 1); a.CE = ce_buf(k - 1);
     a.Ep = e_buf(k); a.CEp = ce_buf(k);
     a.Ah = Ah_.p; a.Bh = Bh_.p; a.Ch = Ch_.p; a.ChT = ChT_.p;
@@ -475,12 +470,11 @@ void Session::launch_k5_any(int k, bool prologue) {
     a.s = scalars(k);
     a.stop = ctrl_;
     a.dense_tiles = dense_tiles();
-    a.rot = rot_;
     if (!prologue) {
         a.side = k5side_;
         k5side_ = SideSolve{};
     }
-    launch_k5(g_, a, prologue, dy_, st_, de_ && !prologue);
+    launch_k5(g_, a, prologue, st_, de_ && !prologue);
 }
 
 // Dense-E mode switch (once per solve).  On data whose outliers are not
@@ -665,8 +659,7 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     // one third of the pools fast, sixteen slow ones in a row are rare).
     // Earlier rounds stay allocated while the next one is drawn, so it gets
     // new pages.
-    const char* pr = std::getenv("TRITD_PROBE_ROUNDS");
-    const int rounds = pr ? std::atoi(pr) : 2;
+    constexpr int rounds = 2;
     // keep room for the chosen pool, the other session buffers and 4 GiB
     const size_t reserve = pool_bytes / 2 + ((size_t)4 << 30);
     std::vector<double*> cand;
@@ -676,7 +669,8 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
         const size_t room = fr > reserve ? (fr - reserve) / pool_bytes : 0;
         if ((size_t)n > room) n = (int)room;
         if (cand.empty() && n < 1) n = 1;  // the pool itself
-        // (hipDeviceMallocContiguous pools probe no differently: tools/contig_probe.py)
+        // (hipDeviceMallocContiguous pools probe no differently:
+        // tools/contig_probe.py at commit 4a7facc)
         for (int c = 0; c < n; ++c) {
             void* p = nullptr;
             if (hipMalloc(&p, pool_bytes) != hipSuccess) {
@@ -704,8 +698,8 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
                         launch_pool_probe32(g_, (float*)f[0], (float*)f[3], (float*)f[4], (float*)f[5],
                                             CE_.f(), st_);
                     else
-                        launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[4],
-                                          (double*)f[5], CE_.p, dy_, st_);
+                        launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[5],
+                                          CE_.p, st_);
                 };
                 probe();  // warm
                 float ms = 1e30f;
@@ -766,39 +760,21 @@ void Session::iterate_overlapped(int k) {
     const int RP = g_.RP;
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
-    // main: M1 -> apply A -> M2 -> apply B -> K2 -> apply C -> K5 -> norms/finish
-    // side: Gram A -> solve B | Gram B -> solve C | Gram C -> solve A(k+1)
-    hipStream_t gs = (ovmode_ >= 3) ? side_ : st_;
-    // per-Gram placement (gram_main_ bit 0: A^TA, 1: B^TB, 2: C^TC on the main
-    // stream): a Gram beside K2/K5 is starved of memory bandwidth (6 us alone,
-    // 50-330 us beside them) and its solve then lands late
-    auto gsel = [&](int bit) { return (gram_main_ >> bit) & 1 ? st_ : gs; };
+    // main: M1 -> apply A -> Gram A -> solve B -> M2 -> apply B -> K2 -> apply C -> K5 -> finish
+    // side: Gram B -> solve C (|| K2) | Gram C -> solve A(k+1) (|| K5)
+    // Gram A^TA and solve B are on the critical path (M2 beside them is only
+    // ~20 us): on the main stream they cost their own time, on the side stream
+    // that plus two cross-stream waits (each widens a kernel boundary by ~6 us)
     do_m1();
     TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
     do_apply_A(GinvA_.p);
-    if (sb_main_ && gs == side_) {
-        // Gram A^TA and solve B are on the critical path (M2 beside them is
-        // only ~20 us): on the main stream they cost their own time, on the
-        // side stream they cost that plus two cross-stream waits (each event
-        // wait or record widens a kernel boundary by ~6 us, measured)
-        launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
-        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
-        do_m2(M2);
-    } else {
-        if (gsel(0) == st_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
-        TRITD_HIP(hipEventRecord(evAtA_, st_));
-        TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
-        if (gsel(0) == side_) launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, side_);
-        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, side_);
-        TRITD_HIP(hipEventRecord(evSB_, side_));
-        do_m2(M2);
-        TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
-    }
+    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+    do_m2(M2);
     do_apply_B(M2, GinvB_.p);
-    if (gsel(1) == st_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
-    if (gsel(1) == side_) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     mark(1);
@@ -806,10 +782,9 @@ void Session::iterate_overlapped(int k) {
     mark(2);
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     do_apply_C(GinvC_.p);
-    if (gsel(2) == st_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-    if (gsel(2) == side_) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/true);
@@ -854,10 +829,9 @@ void Session::iterate_fused(int k) {
     mark(1);
     SideSolve sc;  // update_C's solve (:93 ridge) beside K2
     sc.P = AtA; sc.Q = BtB_.p; sc.alpha = 1e-9; sc.Ginv = GinvC_.p; sc.flags = ctrl_ + 2;
-    sc.R = g_.R; sc.on = k2side_ != 0;
+    sc.R = g_.R; sc.on = 1;
     launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_, 0, -1, sc);
     mark(2);
-    if (!sc.on) solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, st_);
     allreduce(red2_.p, red2_count());
     do_apply_C(GinvC_.p);
     launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
@@ -899,10 +873,9 @@ void Session::iterate_sharded(int k) {
     allreduce(red1_.p, red1_count());
     solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
     do_apply_B(M2, GinvB_.p);
-    if (gram_main_sh_ & 2) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
-    if (!(gram_main_sh_ & 2)) launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     mark(1);
@@ -911,10 +884,9 @@ void Session::iterate_sharded(int k) {
     allreduce(red2_.p, red2_count());
     TRITD_HIP(hipStreamWaitEvent(st_, evSC_, 0));
     do_apply_C(GinvC_.p);
-    if (gram_main_sh_ & 4) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-    if (!(gram_main_sh_ & 4)) launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/false);

@@ -81,7 +81,7 @@ class Session {
     void counters(int64_t* dense_tiles_total, int64_t* tiles_per_launch);
     void k5_profile(int* dense_streams, int* slot_accesses) const {
         // dense-E mode: E^(k), E^(k-1) read and E^(k+1) written densely, no slots
-        *dense_streams = de_ ? 7 : (dy_ ? 4 : 6);
+        *dense_streams = de_ ? 7 : (dy_ ? 4 : 6);  // (fp32: 6, Y_O stored)
         *slot_accesses = de_ ? 0 : (dy_ ? 3 : 2);
     }
     bool dense_e() const { return de_; }
@@ -124,13 +124,12 @@ class Session {
     void iterate_fused(int k);
     bool fused_ = false;
     // K5's norm-partial count (its workgroups; the fp32 rank-split K5 has more)
-    int k5n() const { return f32_ ? k5_parts32(g_) : k5_grid(g_) * k5_tsplit(g_); }
+    int k5n() const { return f32_ ? k5_parts32(g_) : k5_grid(g_) * g_.tsplit; }
     // pairs in red1_'s norm-partial tail: the largest k5n() over the ranks
     // (shards of different heights launch different K5 grids, and every rank
     // must all-reduce the same count); set by agree_counts()
     int k5tail_ = 0;
     void agree_counts();
-    int k2side_ = 1;  // update_C's solve beside K2 (0: after it, experiments)
     SideSolve k5side_;  // the side solve of the next K5 launch
     // communicator: K5's norm partials of iteration pend_k_ wait in red1_'s
     // tail for the next iteration's first all-reduce (one all-reduce fewer
@@ -143,10 +142,6 @@ class Session {
     void create_streams(hipStream_t shared_stream);
     void launch_k5_full(int k, bool fused_finish);
     bool overlap_ = false;
-    int ovmode_ = 2;
-    int gram_main_ = 0, gram_main_sh_ = 0;  // Grams on the main stream (bit 0 A, 1 B, 2 C)
-    bool sb_main_ = true;  // 1-GPU schedule: Gram A^TA and solve B on the main stream
-    int rot_ = 1;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
     hipEvent_t evSA_ = nullptr, evSB_ = nullptr, evSC_ = nullptr;

@@ -87,6 +87,7 @@ SIGNATURES = {
     "tritd_comm_create": (C.c_int, [C.POINTER(vp), vp, i32, i32, i32]),
     "tritd_comm_create_host": (C.c_int, [C.POINTER(vp), ALLREDUCE_FN, vp, i32, i32, i32]),
     "tritd_comm_destroy": (None, [vp]),
+    "tritd_comm_info": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
     "tritd_admm_sharded_virtual_f64": (C.c_int, [vp, i64, i64, i64, i32, C.POINTER(Opts), vp, vp,
                                                  vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32),
                                                  i32]),

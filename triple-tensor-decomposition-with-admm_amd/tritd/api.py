@@ -617,6 +617,13 @@ class Comm:
         check(lib.tritd_comm_unique_id(buf))
         return buf.raw
 
+    def info(self):
+        """(nranks, rank, transport) as the communicator reports them
+        (RCCL: ncclCommCount / ncclCommUserRank); transport 'rccl' or 'host'."""
+        n, me, tr = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib.tritd_comm_info(self.handle, C.byref(n), C.byref(me), C.byref(tr)))
+        return n.value, me.value, ("rccl" if tr.value == 0 else "host")
+
     def close(self):
         if self.handle:
             lib.tritd_comm_destroy(self.handle)
