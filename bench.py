@@ -122,32 +122,41 @@ def end_to_end(tritd, D, r, opts, A0, B0, C0, device):
     return res
 
 
+def latest_profile(name):
+    """The newest profiles/round<N>/<name> (rounds of the driver), or None."""
+    import glob
+    import re
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "round*", name)):
+        m = re.search(r"round(\d+)", f)
+        if m and (best is None or int(m.group(1)) > best[0]):
+            best = (int(m.group(1)), f)
+    return best[1] if best else None
+
+
 def pmc_mfma_util(config):
     """K2's MFMA utilisation from the committed rocprofv3 SQ pass
-    (tools/pmc_summary.py --json -> profiles/*_k2_mfma_util.json):
+    (tools/pmc_summary.py --json -> profiles/round<N>/k2_mfma_util.json):
     SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)."""
-    import glob
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*k2_mfma_util.json"))
-                   if ("_c5_" in os.path.basename(f)) == (config == 5))
-    if not files:
+    f = latest_profile("c5_k2_mfma_util.json" if config == 5 else "k2_mfma_util.json")
+    if not f:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("mfma_util"), os.path.relpath(files[-1], ROOT)
+    with open(f) as fh:
+        d = json.load(fh)
+    return d.get("mfma_util"), os.path.relpath(f, ROOT)
 
 
 def pmc_traffic(config):
     """HBM bytes per fused-update launch from the committed rocprofv3 PMC pass
-    (tools/pmc_traffic.py -> profiles/*_k5_traffic.json, config 5:
-    profiles/*_c5_k5_traffic.json), or None."""
-    import glob
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*k5_traffic.json"))
-                   if ("_c5_" in os.path.basename(f)) == (config == 5))
-    if not files:
+    of the same workload (tools/pmc_traffic.py -> profiles/round<N>/k5_traffic.json,
+    config 5: c5_k5_traffic.json), or None.  rocprofv3 cannot run inside the
+    timed process, so the line cites the committed pass it copies."""
+    f = latest_profile("c5_k5_traffic.json" if config == 5 else "k5_traffic.json")
+    if not f:
         return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    with open(f) as fh:
+        d = json.load(fh)
+    return d.get("bytes_per_launch"), os.path.relpath(f, ROOT)
 
 
 def primitives(device, n=512, r=8, reps=10):

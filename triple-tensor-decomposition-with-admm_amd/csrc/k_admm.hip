@@ -216,12 +216,6 @@ void k5_fused(K5Args a) {
     WT_BEGIN();
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
-    constexpr int LDC = RP + 16; // row stride of the [t][k] C^ slice (2*LDC = 32 mod 64: no bank conflicts)
-    // row stride of the [k][t] slice: odd, so the staging writes (32 lanes of
-    // one t, k = 0, 2, .., 62) fall on distinct banks (stride 16 put them all
-    // on one: 16-way conflicts, ~45 % of K5's LDS cycles); the L-operand
-    // reads then share one bank pair between two lanes (3 LDS cycles, not 2)
-    constexpr int SK = 17;
     const int lane = threadIdx.x & 63;
     // wave-uniform in SGPRs: every tile base below becomes scalar address math
     // (K5 is VALU-issue-bound)
@@ -236,11 +230,24 @@ void k5_fused(K5Args a) {
     const int64_t ntt = a.ntt;
     const int64_t t0 = chunk * ntt / a.tsplit, t1 = (chunk + 1) * ntt / a.tsplit;  // this chunk's t-tiles
 
-    // C^ rows of one t-tile, staged once per workgroup, double-buffered:
-    //   sCT[k][SK]  (L operand: C^(t0+l&15, 4s+(l>>4)))
-    //   sC [16][LDC] (W operand: C^(t0+4r+(l>>4), 16m+(l&15)))
-    __shared__ double sCT[2][RP * SK];
-    __shared__ double sC[2][16 * LDC];
+    // C^ rows of one t-tile, staged once per workgroup in ONE layout read by
+    // both MFMA chains: element (t, k) at t*LDP + 2*(t>>1) + k, LDP = 16 mod
+    // 32 doubles.  ds_read_b64 banks (a/4) mod 64 per 32-lane half
+    // (MI355X_MICROARCH.md §LDS): the L operand (t = l&15, k = 4s+(l>>4)) and
+    // the W operand (t = 4r+(l>>4), k = 16m+(l&15)) both touch 32 distinct
+    // bank pairs per half, and the staging ds_write_b128 8 distinct 16-B
+    // slots per 8-lane group; every operand address is a per-lane base plus
+    // an immediate.  Four buffers, staged SD = 2 t-tiles ahead, so a barrier
+    // closes every second t-tile only (the buffer a step stages was read two
+    // steps earlier, and is read two steps later).  Round 4, against round 3's
+    // two layouts ([t][k] and [k][t] copies, double-buffered, a barrier per
+    // t-tile): K5 0.960 -> 0.924 ms, iteration 1.366 -> 1.330 ms (6
+    // interleaved pairs, profiles/round4/ab_k5_one_layout.txt).
+    constexpr int LDP = ((RP + 31) / 32) * 32 + 16;
+    constexpr int SLICE = 16 * LDP + 16;
+    constexpr int NBUF = 4, SD = 2;
+    __shared__ __attribute__((aligned(16))) double sCS[NBUF][SLICE];
+    auto slice_buf = [](int64_t s) { return (int)(s & (NBUF - 1)); };
     // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
     __shared__ double tsm[K5_WAVES][16 * 17];
     double* ts = tsm[wid];
@@ -268,13 +275,15 @@ void k5_fused(K5Args a) {
             const int e = threadIdx.x + q * 64 * K5_WAVES;
             if (SP % (64 * K5_WAVES) == 0 || e < SP) {
                 const int row = (2 * e) / RP, k = (2 * e) % RP;
-                sC[buf][row * LDC + k] = sv[q][0];
-                sC[buf][row * LDC + k + 1] = sv[q][1];
-                sCT[buf][k * SK + row] = sv[q][0];
-                sCT[buf][(k + 1) * SK + row] = sv[q][1];
+                *reinterpret_cast<d2v*>(&sCS[buf][row * LDP + 2 * (row >> 1) + k]) = sv[q];
             }
         }
     };
+    // operand reads: L (t = il, k = 4s+tg) and W (t = 4r+tg, k = 16m+il)
+    const int offL = il * LDP + 2 * (il >> 1) + tg;
+    const int offW = tg * LDP + 2 * (tg >> 1) + il;
+    auto opL = [&](int buf, int s) { return sCS[buf][offL + 4 * s]; };
+    auto opW = [&](int buf, int r, int m) { return sCS[buf][offW + r * (4 * LDP + 4) + 16 * m]; };
 
     // the Khatri-Rao operand of this ij-tile: KR(ij, 4s+tg) (CP or Qi, kernels.h)
     double kr[KS];
@@ -325,8 +334,8 @@ void k5_fused(K5Args a) {
     // every __shared__ array of this kernel, in bytes (160 KiB per CU; RP =
     // 256 at one wave per SIMD is the largest: ~147 KB)
     constexpr size_t LDS_BYTES =
-        sizeof(double) * (2 * RP * SK + 2 * 16 * LDC + K5_WAVES * 16 * 17 + K5_WAVES * 96 +
-                          (NIMG > 0 ? K5_WAVES * NIMG : 1) * CE_IMG + 2 * K5_WAVES);
+        sizeof(double) * (NBUF * SLICE + K5_WAVES * 16 * 17 +
+                          K5_WAVES * 96 + (NIMG > 0 ? K5_WAVES * NIMG : 1) * CE_IMG + 2 * K5_WAVES);
     static_assert(LDS_BYTES <= 160 * 1024, "k5_fused: LDS over the 160 KiB of a CU");
     // D, Y_L, T (PRO: O) through buffer descriptors based at this wave's first
     // tile: the t-tile offset is a scalar (soffset), the lane offset a
@@ -379,26 +388,23 @@ void k5_fused(K5Args a) {
 
     // one t-tile: cx holds its data, `buf` its C^ slice; if `pf`, tile tt+1 is
     // prefetched into nx and its C^ slice staged into buf^1
-    auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf) {
+    // one t-tile: cx holds its data; pf: tile tt+1 is loaded into nx; ps: the
+    // C^ slice SD t-tiles ahead is staged; bar: the step ends at a barrier
+    auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf, bool ps, bool bar) {
         const int64_t o = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
-        // prefetch first; it only needs tile tt+1's dense flag, whose slot
-        // arrived with the batch of this tile
+        // prefetch first
+        if (ps) stage_load(tt + SD);
         if (pf) {
-            stage_load(tt + 1);
             load(tt + 1, nx);
             if constexpr (DE) {  // both E tiles are part of the regular batch
                 load_dense(tt + 1, nx);
                 load_dense_p(tt + 1, nx);
             }
-            // keep the prefetch ahead of the compute: the scheduler otherwise
-            // sinks it next to the stores (less register pressure, no latency
-            // hiding)
-            __builtin_amdgcn_sched_barrier(0);
-            // rare, wave-uniform: tile tt+1 overflowed last time.  Issued after
-            // the batch and consumed a step later, so the common path's waits
-            // stay exact
-
         }
+        // keep the prefetch ahead of the compute: the scheduler otherwise
+        // sinks it next to the stores (less register pressure, no latency
+        // hiding)
+        __builtin_amdgcn_sched_barrier(0);
         double ev[4], evp[4];
         if constexpr (DE) {
 #pragma unroll
@@ -433,7 +439,6 @@ void k5_fused(K5Args a) {
             }
             if (pf) load_slot(tt + 2, cx);  // cx.ce and cx.cep were consumed above
         }
-        const double* cR = sC[buf];
         double tr[4];
         if constexpr (PRO) {
 #pragma unroll
@@ -445,10 +450,9 @@ void k5_fused(K5Args a) {
                 }
         } else {
             // L^T(t, ij) of this t-tile: KS dependent MFMAs
-            const double* cT = sCT[buf];
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int s = 0; s < KS; ++s) lacc = mfma4(cT[(4 * s + tg) * SK + il], kr[s], lacc);
+            for (int s = 0; s < KS; ++s) lacc = mfma4(opL(buf, s), kr[s], lacc);
             double En[4];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
@@ -518,11 +522,12 @@ void k5_fused(K5Args a) {
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int m = 0; m < MT; ++m)
-                wacc[m] = mfma4(cR[(4 * r + tg) * LDC + 16 * m + il], tr[r], wacc[m]);
-        if (pf) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
-        __syncthreads();  // C^ buffer `buf` and the T transpose buffer are free again
+                wacc[m] = mfma4(opW(buf, r, m), tr[r], wacc[m]);
+        // the slice SD t-tiles ahead into the buffer read SD t-tiles ago
+        if (ps) stage_store(slice_buf(tt + SD - t0));
+        if (bar) __syncthreads();
         // step boundary: the scheduler would otherwise hoist the next step's
-        // dense-slot test (which needs this step's loads) above the barrier
+        // work above the barrier
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -540,20 +545,26 @@ void k5_fused(K5Args a) {
         load_dense(t0, xa);
         load_dense_p(t0, xa);
     }
-    stage_load(t0);
-    stage_store(0);
+    for (int64_t q = 0; q < SD; ++q) {  // the first SD slices
+        if (t0 + q < t1) {
+            stage_load(t0 + q);
+            stage_store(slice_buf(q));
+        }
+    }
     __syncthreads();
     int64_t tt = t0;
-    int b = 0;  // buffer of t-tile tt's C^ slice
-    for (; tt + 2 < t1; tt += 2) {
-        body(tt, b, xa, xb, true);
-        body(tt + 1, b ^ 1, xb, xa, true);
+    // steps in pairs (the register sets alternate by name; every flag is a
+    // constant inside the loop); with SD = 2 only the second step of a pair
+    // ends at a barrier
+    for (; tt + 3 < t1; tt += 2) {
+        body(tt, slice_buf(tt - t0), xa, xb, true, true, false);
+        body(tt + 1, slice_buf(tt + 1 - t0), xb, xa, true, true, true);
     }
-    if (tt + 1 < t1) {
-        body(tt, b, xa, xb, true);
-        body(tt + 1, b ^ 1, xb, xa, false);
-    } else {
-        body(tt, b, xa, xb, false);
+    {
+        const int64_t rem = t1 - tt;  // 1..3 steps left
+        body(tt, slice_buf(tt - t0), xa, xb, rem > 1, rem > SD, false);
+        if (rem > 1) body(tt + 1, slice_buf(tt + 1 - t0), xb, xa, rem > 2, rem > 1 + SD, rem > 2);
+        if (rem > 2) body(tt + 2, slice_buf(tt + 2 - t0), xa, xb, false, false, false);
     }
     // Epilogue lane values recomputed here from threadIdx (opaque to the
     // compiler): otherwise it hoists the W addresses and lane tests above the
@@ -667,7 +678,10 @@ void launch_k5(const Geom& g, const K5Args& a, bool prologue, hipStream_t st, bo
     }
 #undef K5_CASE
     TRITD_CHECK_LAUNCH();
-    if (b.tsplit > 1) {
+    // a t-split walk leaves W as partial sets: the CP model's M1 / M2 sum them
+    // as they read W (k_contract.hip); the Qi model's contractions read one W,
+    // summed here in set order
+    if (b.tsplit > 1 && a.ahj != 0) {
         const int64_t stride = (int64_t)g.RP * g.plane;
         hipLaunchKernelGGL(k_w_reduce, dim3((unsigned)std::min<int64_t>(cdiv(stride, 256), 2048)),
                            dim3(256), 0, st, b.Wk, stride, b.tsplit, b.stop);

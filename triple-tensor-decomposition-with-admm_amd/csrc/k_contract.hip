@@ -38,11 +38,14 @@ __device__ __forceinline__ d4 mfma4(double a, double b, d4 c) {
 // ticket, cost more than it saved: the device-scope fences it needs write
 // back and invalidate L2 on gfx950 and slowed every following kernel.)
 // ---------------------------------------------------------------------------
-template <int M1_WAVES>
+// SETS > 1: W arrives as the partial sets of a t-split K5 walk (k5_tsplit,
+// set c at Wk + c*sstride) and is summed here in set order — the same
+// additions, in the same order, as the separate reduction launch it replaces.
+template <int M1_WAVES, bool SETS>
 __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__ Wk,
                                                       const double* __restrict__ Bh, double* M1,
                                                       int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                                      const int* stop) {
+                                                      const int* stop, int sets, int64_t sstride) {
     if (*stop) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * 64 + lane;
@@ -54,12 +57,18 @@ __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__
     if (i < n1p) {
         const double* wp = Wk + (int64_t)k * plane + i;
         const double* bp = Bh + k;
+        auto wv = [&](int64_t o) {
+            double x = wp[o];
+            if constexpr (SETS)
+                for (int c = 1; c < sets; ++c) x += wp[c * sstride + o];
+            return x;
+        };
         int64_t j = w;
         for (; j + 7 * JS < n2; j += 8 * JS) {  // 8 independent chains, j = w + JS*u
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] = fma(wp[(j + JS * u) * n1p], bp[(j + JS * u) * RP], acc[u]);
+            for (int u = 0; u < 8; ++u) acc[u] = fma(wv((j + JS * u) * n1p), bp[(j + JS * u) * RP], acc[u]);
         }
-        for (; j < n2; j += JS) acc[0] = fma(wp[j * n1p], bp[j * RP], acc[0]);
+        for (; j < n2; j += JS) acc[0] = fma(wv(j * n1p), bp[j * RP], acc[0]);
     }
     __shared__ double red[JS][64];
     red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
@@ -79,12 +88,16 @@ void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, co
     // (16-byte-load variants, two rows per lane, measured neutral or slower
     // in the solver: DESIGN.md §4)
     const dim3 grid((unsigned)cdiv(g.n1p, 64), g.RP);
-    if (g.n1p >= 256)  // (two rows per lane with 16-B loads halves the waves: 72 vs 36 us)
-        hipLaunchKernelGGL(k_m1<4>, grid, dim3(64 * 4), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
-                           g.RP, stop);
-    else
-        hipLaunchKernelGGL(k_m1<16>, grid, dim3(64 * 16), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane,
-                           g.RP, stop);
+    const int sets = g.tsplit;
+    const int64_t ss = (int64_t)g.RP * g.plane;
+#define M1_LAUNCH(NW, S) \
+    hipLaunchKernelGGL((k_m1<NW, S>), grid, dim3(64 * NW), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop, sets, ss)
+    if (g.n1p >= 256) {  // (two rows per lane with 16-B loads halves the waves: 72 vs 36 us)
+        if (sets > 1) M1_LAUNCH(4, true); else M1_LAUNCH(4, false);
+    } else {
+        if (sets > 1) M1_LAUNCH(16, true); else M1_LAUNCH(16, false);
+    }
+#undef M1_LAUNCH
     TRITD_CHECK_LAUNCH();
 }
 
@@ -100,11 +113,12 @@ void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, co
 #ifndef TRITD_M2_NW
 #define TRITD_M2_NW 8
 #endif
-template <int RP, int NWV>
+template <int RP, int NWV, bool SETS = false>
 __global__ __launch_bounds__(64 * NWV) void k_m2(const double* __restrict__ Wk,
                                                  const double* __restrict__ AhT, double* M2,
                                                  int64_t n1p, int64_t n2, int64_t plane,
-                                                 const int* stop, SideSolve side) {
+                                                 const int* stop, SideSolve side, int sets,
+                                                 int64_t sstride) {
     if (*stop) return;
     if constexpr (RP <= 64 && RP % NWV == 0) {
         if (side.on && blockIdx.x == 0) {
@@ -123,7 +137,10 @@ __global__ __launch_bounds__(64 * NWV) void k_m2(const double* __restrict__ Wk,
     const d2v* ap = reinterpret_cast<const d2v*>(AhT + (int64_t)k * n1p);
     double a0 = 0.0, a1 = 0.0;
     for (int64_t q = lane; q < (n1p >> 1); q += 64) {
-        const d2v x = wp[q], y = ap[q];
+        d2v x = wp[q];
+        const d2v y = ap[q];
+        if constexpr (SETS)  // t-split partial sets of W, summed in set order (k_m1)
+            for (int c = 1; c < sets; ++c) x += wp[c * (sstride >> 1) + q];
         a0 = fma(x.x, y.x, a0);
         a1 = fma(x.y, y.y, a1);
     }
@@ -142,13 +159,25 @@ void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, c
     if (side.on && (g.RP > 64 || g.RP % NV != 0))
         throw Error(TRITD_ERR_ARG, "M2 side solve: RP <= 64 and a multiple of TRITD_M2_NW only");
     const dim3 grid((unsigned)(g.n2 * cdiv(g.RP, NV) + side.on)), blk(64 * NV);
+    const int sets = g.tsplit;
+    const int64_t ss = (int64_t)g.RP * g.plane;
+#define M2_CASE(RPV)                                                                                  \
+    case RPV:                                                                                         \
+        if (sets > 1)                                                                                 \
+            hipLaunchKernelGGL((k_m2<RPV, NV, true>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, \
+                               stop, side, sets, ss);                                                 \
+        else                                                                                          \
+            hipLaunchKernelGGL((k_m2<RPV, NV, false>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, \
+                               stop, side, sets, ss);                                                 \
+        break;
     switch (g.RP) {
-        case 16: hipLaunchKernelGGL((k_m2<16, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 32: hipLaunchKernelGGL((k_m2<32, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 48: hipLaunchKernelGGL((k_m2<48, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 64: hipLaunchKernelGGL((k_m2<64, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 128: hipLaunchKernelGGL((k_m2<128, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
-        case 256: hipLaunchKernelGGL((k_m2<256, NV>), grid, blk, 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, stop, side); break;
+        M2_CASE(16)
+        M2_CASE(32)
+        M2_CASE(48)
+        M2_CASE(64)
+        M2_CASE(128)
+        M2_CASE(256)
+#undef M2_CASE
         default: throw Error(TRITD_ERR_UNSUPPORTED, "M2: RP not supported");
     }
     TRITD_CHECK_LAUNCH();
@@ -1142,6 +1171,130 @@ void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, dou
         default: throw Error(TRITD_ERR_UNSUPPORTED, "apply: RP not supported");
     }
 #undef APPLY_CASE
+    TRITD_CHECK_LAUNCH();
+}
+
+// ---------------------------------------------------------------------------
+// Small problems: Y = M * Ginv and G = Y^T Y in ONE workgroup (one launch
+// instead of k_apply + k_gram).  The ADMM iteration applies and Grams each
+// factor back to back (update_A/B/C, triple_decomp_ADMM.m:77-81,86-88,93-95);
+// at the sensor shape (config 2: 64 / 4 / 1152 rows, RP 32) each of those
+// launches is a few microseconds of dispatch and ramp around a fraction of a
+// microsecond of work.  Rows are taken in chunks of 64: the 4 waves form the
+// chunk's 16 x 16 tiles of Y (f64 MFMA, Ginv staged in LDS), store Y / Y^T
+// and the chunk to LDS, then accumulate their tiles of G over it.  The sums
+// run over rows in chunk order, a fixed order (not k_gram's): results agree
+// to rounding.  The pinv fallback (pinv.h) runs once, in this workgroup.
+// ---------------------------------------------------------------------------
+template <int RP>
+__global__ __launch_bounds__(256) void k_apply_gram(const double* __restrict__ M, int64_t rows,
+                                                    const double* __restrict__ Ginv, double* Y,
+                                                    double* YT, int64_t ldT, double* G,
+                                                    const int* stop, int* flags) {
+    if (stop && *stop) return;
+    constexpr int NT = 256, NCT = RP / 16, KS = RP / 4;
+    constexpr int LD = ((RP + 31) / 32) * 32 + 16;  // = 16 mod 32: conflict-free operand reads
+    constexpr int LDP = RP + 1;                     // jacobi_pinv's own stride
+    constexpr int UN = (2 * RP * LDP > 64 * LD) ? 2 * RP * LDP : 64 * LD;
+    __shared__ double Gl[RP * LD];
+    __shared__ double un[UN];  // pA | pV of the pinv fallback, then the Y chunk
+    __shared__ double rot[RP], red[NT / 64 + RP];
+    __shared__ int pq[RP];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m = lane & 15, kq = lane >> 4;
+    const double req = Ginv[ginv_req(RP)];
+    if (req != 0.0) {
+        double* pA = un;
+        double* pV = un + RP * LDP;
+        for (int e = tid; e < RP * RP; e += NT) {
+            const int i = e / RP, j = e - (e / RP) * RP;
+            pA[i * LDP + j] = Ginv[(int64_t)RP * RP + e];
+        }
+        __syncthreads();
+        jacobi_pinv<RP, NT>(pA, pV, LDP, (int)req, Gl, LD, rot, pq, red, flags);
+    } else {
+        for (int e = tid; e < RP * RP; e += NT) {
+            const int i = e / RP, j = e - (e / RP) * RP;
+            Gl[i * LD + j] = Ginv[e];
+        }
+    }
+    __syncthreads();
+    double* Ys = un;
+    constexpr int GT = NCT * NCT, GPW = (GT + 3) / 4;  // Gram tiles, per wave
+    d4 gacc[GPW];
+#pragma unroll
+    for (int q = 0; q < GPW; ++q) gacc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int64_t c0 = 0; c0 < rows; c0 += 64) {
+        // Y tiles (rt, ct) of this chunk, wave w takes ids w, w+4, ...
+        for (int id = w; id < 4 * NCT; id += 4) {
+            const int rt = id / NCT, ct = id - (id / NCT) * NCT;
+            const int64_t r0 = c0 + 16 * rt;
+            const bool in = r0 + m < rows;
+            const double* mp = M + (in ? (r0 + m) * RP : 0) + kq;
+            double a[KS];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) a[s] = in ? mp[4 * s] : 0.0;
+            d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) acc = mfma4(a[s], Gl[(4 * s + kq) * LD + 16 * ct + m], acc);
+            // C/D element r of lane l: Y(r0 + (l>>4) + 4r, 16ct + (l&15))
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rl = 16 * rt + kq + 4 * r;
+                const int64_t i = c0 + rl;
+                Ys[rl * LD + 16 * ct + m] = acc[r];  // zero for rows past the end
+                if (i < rows) {
+                    Y[i * RP + 16 * ct + m] = acc[r];
+                    if (YT) YT[(int64_t)(16 * ct + m) * ldT + i] = acc[r];
+                }
+            }
+        }
+        __syncthreads();
+        // G(ta, tb) += sum over the chunk's 64 rows: 16 K-steps of 4 rows
+#pragma unroll
+        for (int q = 0; q < GPW; ++q) {
+            const int id = w + 4 * q;
+            if (id < GT) {
+                const int ta = id / NCT, tb = id - (id / NCT) * NCT;
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                    gacc[q] = mfma4(Ys[(4 * s + kq) * LD + 16 * ta + m], Ys[(4 * s + kq) * LD + 16 * tb + m],
+                                    gacc[q]);
+            }
+        }
+        __syncthreads();  // the chunk buffer is rewritten next
+    }
+#pragma unroll
+    for (int q = 0; q < GPW; ++q) {
+        const int id = w + 4 * q;
+        if (id < GT) {
+            const int ta = id / NCT, tb = id - (id / NCT) * NCT;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) G[(int64_t)(16 * ta + kq + 4 * r) * RP + 16 * tb + m] = gacc[q][r];
+        }
+    }
+}
+
+bool apply_gram_small(int RP, int64_t rows) {
+    // one CU's f64 MFMA against two launches of a few us each: worth it while
+    // rows * RP^2 stays under ~5 us of one CU (config 3's largest factor)
+    return RP <= 64 && (double)rows * RP * RP <= 327680.0;
+}
+
+void launch_apply_gram(int RP, const double* M, int64_t rows, const double* Ginv, double* Y,
+                       double* YT, int64_t ldT, double* G, const int* stop, int* flags,
+                       hipStream_t st) {
+    if (!apply_gram_small(RP, rows)) throw Error(TRITD_ERR_ARG, "apply+Gram: problem too large for one workgroup");
+#define AG_CASE(RPV) \
+    case RPV: hipLaunchKernelGGL(k_apply_gram<RPV>, dim3(1), dim3(256), 0, st, M, rows, Ginv, Y, YT, ldT, G, stop, flags); break;
+    switch (RP) {
+        AG_CASE(16)
+        AG_CASE(32)
+        AG_CASE(48)
+        AG_CASE(64)
+        default: throw Error(TRITD_ERR_UNSUPPORTED, "apply+Gram: RP not supported");
+    }
+#undef AG_CASE
     TRITD_CHECK_LAUNCH();
 }
 

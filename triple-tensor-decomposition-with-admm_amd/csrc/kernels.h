@@ -116,6 +116,11 @@ void launch_solve(int RP, int R, const double* P, const double* Q, double alpha,
 // Y = M * Ginv ([rows][RP]); optional transposed copy YT[k*ldT + i].  A set
 // request word makes every workgroup use pinv(saved Gram) instead (pinv.h);
 // flags[0] is raised when that pinv drops a singular value.
+// Y = M * Ginv and G = Y^T Y in one workgroup (small problems: apply_gram_small)
+bool apply_gram_small(int RP, int64_t rows);
+void launch_apply_gram(int RP, const double* M, int64_t rows, const double* Ginv, double* Y,
+                       double* YT, int64_t ldT, double* G, const int* stop, int* flags,
+                       hipStream_t st);
 void launch_apply(int RP, const double* M, int64_t rows, const double* Ginv, double* Y, double* YT,
                   int64_t ldT, const int* stop, int* flags, hipStream_t st);
 // ---- Qi model (opts.model='qi', k_qi.hip; origin_triple_tensor/build{F,G,H}.m) ----

@@ -438,6 +438,40 @@ void Session::do_apply_C(double* Ginv) {
         launch_apply(g_.RP, red2_.p, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ctrl_, ctrl_ + 2, st_);
 }
 
+// apply + Gram of one factor (update_A/B/C, :77-81,86-88,93-95): one launch
+// for small fp64 problems (k_apply_gram), else k_apply then k_gram
+bool Session::small_ag(int64_t rows) const {
+    return !f32_ && !qi_ && g_.RP <= 64 && apply_gram_small(g_.RP, rows);
+}
+
+void Session::apply_gram_A(double* AtA) {
+    if (small_ag(g_.n1p)) {
+        launch_apply_gram(g_.RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, AtA, ctrl_, ctrl_ + 2, st_);
+        return;
+    }
+    do_apply_A(GinvA_.p);
+    launch_gram(g_.RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+}
+
+void Session::apply_gram_B(const double* M2) {
+    if (small_ag(g_.n2)) {
+        launch_apply_gram(g_.RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, BtB_.p, ctrl_, ctrl_ + 2, st_);
+        return;
+    }
+    do_apply_B(M2, GinvB_.p);
+    launch_gram(g_.RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+}
+
+void Session::apply_gram_C() {
+    if (small_ag(g_.n3p)) {
+        launch_apply_gram(g_.RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, CtC_.p, ctrl_, ctrl_ + 2,
+                          st_);
+        return;
+    }
+    do_apply_C(GinvC_.p);
+    launch_gram(g_.RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+}
+
 void Session::launch_k5_any(int k, bool prologue) {
     if (f32_) {
         K5Args32 a{};
@@ -607,8 +641,7 @@ void Session::phaseA(int k) {
     double* AtA = red1_.p + g_.n2 * RP;
     do_m1();
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, st_);
-    do_apply_A(GinvA_.p);
-    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    apply_gram_A(AtA);
     do_m2(M2);
 }
 
@@ -618,8 +651,7 @@ void Session::phaseB(int k) {
     const double* M2 = red1_.p;
     const double* AtA = red1_.p + g_.n2 * RP;
     solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
-    do_apply_B(M2, GinvB_.p);
-    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    apply_gram_B(M2);
     mark(1);
     do_m3();
     mark(2);
@@ -629,8 +661,7 @@ void Session::phaseC(int k) {
     const int RP = g_.RP;
     const double* AtA = red1_.p + g_.n2 * RP;
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, st_);  // :93 ridge
-    do_apply_C(GinvC_.p);
-    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    apply_gram_C();
     launch_k5_full(k, /*fused_finish=*/false);
 }
 
@@ -801,8 +832,7 @@ void Session::iterate_fused(int k) {
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
     do_m1();
-    do_apply_A(GinvA_.p);
-    launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    apply_gram_A(AtA);
     if (comm_ && comm_->active()) {
         do_m2(M2);
         // M1 .. M2 above ran before the stop test of iteration k-1: they
@@ -824,8 +854,7 @@ void Session::iterate_fused(int k) {
         sb.R = g_.R; sb.on = 1;
         launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_, sb);
     }
-    do_apply_B(M2, GinvB_.p);
-    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    apply_gram_B(M2);
     mark(1);
     SideSolve sc;  // update_C's solve (:93 ridge) beside K2
     sc.P = AtA; sc.Q = BtB_.p; sc.alpha = 1e-9; sc.Ginv = GinvC_.p; sc.flags = ctrl_ + 2;
@@ -833,8 +862,7 @@ void Session::iterate_fused(int k) {
     launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_, 0, -1, sc);
     mark(2);
     allreduce(red2_.p, red2_count());
-    do_apply_C(GinvC_.p);
-    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    apply_gram_C();
     // the next update_A's solve (B^TB, C^TC of this iteration) beside K5
     k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;
     k5side_.flags = ctrl_ + 2; k5side_.R = g_.R; k5side_.on = 1;
