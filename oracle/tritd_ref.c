@@ -157,6 +157,7 @@ static void gram_ffT(const double* F, int R, idx K, double alpha, double* G) {
         for (int t = 0; t < nt; ++t) s += part[(idx)t * R * R + e];
         G[e] = s;
     }
+    free(part);  /* (leaked until round 4: found by the ASan build, tests/test_sanitizers.py) */
     for (int k = 0; k < R; ++k) G[k + (idx)R * k] += alpha;
 }
 

@@ -98,13 +98,15 @@ int mexAtExit(void (*fn)(void)) {
 
 static mxArray* sgl(const float* p, std::vector<mwSize> dims) {
     mxArray* a = mxCreateNumericArray(dims.size(), dims.data(), mxSINGLE_CLASS, mxREAL);
-    std::memcpy(a->fdata.data(), p, a->fdata.size() * sizeof(float));
+    if (!a->fdata.empty()) std::memcpy(a->fdata.data(), p, a->fdata.size() * sizeof(float));
     return a;
 }
 
 static mxArray* dbl(const double* p, std::vector<mwSize> dims) {
     mxArray* a = mxCreateNumericArray(dims.size(), dims.data(), mxDOUBLE_CLASS, mxREAL);
-    std::memcpy(a->data.data(), p, a->data.size() * sizeof(double));
+    // (an empty array may come with a null pointer: memcpy's arguments must
+    // not be null even for zero bytes — UBSan, tests/test_sanitizers.py)
+    if (!a->data.empty()) std::memcpy(a->data.data(), p, a->data.size() * sizeof(double));
     return a;
 }
 

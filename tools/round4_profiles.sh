@@ -27,3 +27,8 @@ cut -c1-400 profiles/round4/bench_line.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prims_stats -o run -- \
     python3 tools/bench_prims.py > profiles/round4/prims.json 2> $O/prims.err || exit $?
 find $O/stats $O/prims_stats -name "*kernel_stats.csv" | head -3
+if [ -n "${SMALL:-}" ]; then
+  timeout -k 10 300 python3 bench.py --config 2 --no-e2e --no-prims > profiles/round4/c2_bench_line.json 2> $O/c2.err || exit $?
+  timeout -k 10 300 python3 bench.py --config 3 --no-e2e --no-prims > profiles/round4/c3_bench_line.json 2> $O/c3.err || exit $?
+  cut -c1-200 profiles/round4/c2_bench_line.json profiles/round4/c3_bench_line.json
+fi

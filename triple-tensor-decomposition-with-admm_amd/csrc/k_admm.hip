@@ -71,6 +71,9 @@ static constexpr int K5_WPE = 2;
 // stores: round 2 interleaved A/B, nt stores -1.5 % iteration, nt loads a
 // further -0.9 % (M1 then finds W still in the Infinity Cache).
 static constexpr int K5_NT_AUX = 2;
+#ifndef K5_ORD
+#define K5_ORD 0  // experiment: dense-E branch after the L MFMAs, E encode after the W MFMAs
+#endif
 
 #if TRITD_WTRACE
 WT_DECL(g_wt_k5)
@@ -388,6 +391,25 @@ void k5_fused(K5Args a) {
 
     // one t-tile: cx holds its data, `buf` its C^ slice; if `pf`, tile tt+1 is
     // prefetched into nx and its C^ slice staged into buf^1
+    // rare, wave-uniform: an overflowed tile's values are in the dense buffer,
+    // loaded when met (a wait on this wave's outstanding loads).  Round 4: the
+    // same speed as prefetching them into two more register sets one step
+    // ahead (K5 0.949 vs 0.949 ms, 6 interleaved pairs), without that form's
+    // 11 spilled VGPRs.
+    auto dense_fix = [&](int64_t tt, bool dn, bool dp, double (&ev)[4], double (&evp)[4]) {
+        if (dn || dp) {
+            const int64_t od = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
+            const d2v a0 = E2[od], a1 = E2[od + 64], b0 = Ep2[od], b1 = Ep2[od + 64];
+            ev[0] = dn ? a0[0] : ev[0];
+            ev[1] = dn ? a0[1] : ev[1];
+            ev[2] = dn ? a1[0] : ev[2];
+            ev[3] = dn ? a1[1] : ev[3];
+            evp[0] = dp ? b0[0] : evp[0];
+            evp[1] = dp ? b0[1] : evp[1];
+            evp[2] = dp ? b1[0] : evp[2];
+            evp[3] = dp ? b1[1] : evp[3];
+        }
+    };
     // one t-tile: cx holds its data; pf: tile tt+1 is loaded into nx; ps: the
     // C^ slice SD t-tiles ahead is staged; bar: the step ends at a barrier
     auto body = [&](int64_t tt, int buf, Regs& cx, Regs& nx, bool pf, bool ps, bool bar) {
@@ -406,6 +428,7 @@ void k5_fused(K5Args a) {
         // hiding)
         __builtin_amdgcn_sched_barrier(0);
         double ev[4], evp[4];
+        bool dn = false, dp = false;
         if constexpr (DE) {
 #pragma unroll
             for (int p = 0; p < 2; ++p)
@@ -418,28 +441,12 @@ void k5_fused(K5Args a) {
             // (selects, not a branch, for a dense tile: a branch would cut the
             // basic block and keep the scheduler from interleaving the decode
             // with the L MFMAs)
-            const bool dn = ce_decode(cx.ce, lane, img, ev);
-            const bool dp = ce_decode(cx.cep, lane, imgp, evp);
-            // rare, wave-uniform: an overflowed tile's values are in the dense
-            // buffer, loaded here when met (a wait on this wave's outstanding
-            // loads).  Round 4: the same speed as prefetching them into two
-            // more register sets one step ahead (K5 0.949 vs 0.949 ms, 6
-            // interleaved pairs), without that form's 11 spilled VGPRs.
-            if (dn || dp) {
-                const int64_t od = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
-                const d2v a0 = E2[od], a1 = E2[od + 64], b0 = Ep2[od], b1 = Ep2[od + 64];
-                ev[0] = dn ? a0[0] : ev[0];
-                ev[1] = dn ? a0[1] : ev[1];
-                ev[2] = dn ? a1[0] : ev[2];
-                ev[3] = dn ? a1[1] : ev[3];
-                evp[0] = dp ? b0[0] : evp[0];
-                evp[1] = dp ? b0[1] : evp[1];
-                evp[2] = dp ? b1[0] : evp[2];
-                evp[3] = dp ? b1[1] : evp[3];
-            }
+            dn = ce_decode(cx.ce, lane, img, ev);
+            dp = ce_decode(cx.cep, lane, imgp, evp);
+            if (!K5_ORD) dense_fix(tt, dn, dp, ev, evp);
             if (pf) load_slot(tt + 2, cx);  // cx.ce and cx.cep were consumed above
         }
-        double tr[4];
+        double tr[4], En[4];
         if constexpr (PRO) {
 #pragma unroll
             for (int p = 0; p < 2; ++p)
@@ -453,7 +460,9 @@ void k5_fused(K5Args a) {
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int s = 0; s < KS; ++s) lacc = mfma4(opL(buf, s), kr[s], lacc);
-            double En[4];
+            // (K5_ORD: the decode's LDS round trips share a basic block with
+            // the L MFMAs; the rare dense branch follows them)
+            if (K5_ORD && !DE) dense_fix(tt, dn, dp, ev, evp);
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 d2v YLn2;
@@ -500,7 +509,7 @@ void k5_fused(K5Args a) {
                 __builtin_nontemporal_store(d2v{En[0], En[1]}, Ep2 + o);
                 __builtin_nontemporal_store(d2v{En[2], En[3]}, Ep2 + o + 64);
                 ++ndense;
-            } else {
+            } else if (!K5_ORD) {
                 ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
             }
         }
@@ -523,6 +532,9 @@ void k5_fused(K5Args a) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
                 wacc[m] = mfma4(opW(buf, r, m), tr[r], wacc[m]);
+        // (K5_ORD: the encode's LDS round trips after the W MFMAs, its rare
+        // dense-store branch last)
+        if constexpr (K5_ORD && !PRO && !DE) ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
         // the slice SD t-tiles ahead into the buffer read SD t-tiles ago
         if (ps) stage_store(slice_buf(tt + SD - t0));
         if (bar) __syncthreads();

@@ -440,7 +440,7 @@ void k5_f32(K5Args32 a) {
 template <int RP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k5_f32s(K5Args32 a) {
-    static_assert(RP % 128 == 0, "k5_f32s: RP = 128 or 256");
+    static_assert(RP == 256, "k5_f32s: RP = 256 (the L-read permutation assumes 4 granules per group)");
     if (*a.stop) return;
     constexpr int KS = RP / 4, MT = RP / 16, LDC = RP + 4;
     constexpr int G = MT / 4, GH = G / 2, KSH = KS / 2, MTH = MT / 2;
@@ -524,11 +524,18 @@ void k5_f32s(K5Args32 a) {
         constexpr int h = decltype(HC)::value;
         constexpr int NKR = KSH;  // KR operands this wave holds
         constexpr int NWT = MTH;  // W M-tiles this wave accumulates
-        // KR(ij = l & 15, k = (l>>4) * KS + h*KSH + s), single-rounded
+        // KR(ij = l & 15, k), single-rounded, for the k this lane's L read
+        // takes at slot s = 4 s4 + u: granule s4 of its half, permuted within
+        // each group of 4 granules by the lane's K group tg (sig below), so
+        // that the 16 lanes of a ds_read_b128 group hit 16 distinct 16-B bank
+        // slots (the unpermuted order was 2-way conflicted: the gran rotation
+        // below depends on tg).  Every k is still taken once; only which k
+        // share an MFMA changes (the f32 sum of L is formed in another order).
+        auto sig = [&](int s4) { return 4 * (s4 >> 2) + (((s4 & 3) - tg) & 3); };
         float kr[NKR];
 #pragma unroll
         for (int s = 0; s < NKR; ++s) {
-            const int k = tg * KS + h * KSH + s;
+            const int k = tg * KS + h * KSH + 4 * sig(s >> 2) + (s & 3);
             kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
         }
 #pragma unroll
@@ -578,8 +585,9 @@ void k5_f32s(K5Args32 a) {
                 for (int q = 0; q < 4; ++q) lacc[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
                 for (int s4 = 0; s4 < KSH / 4; ++s4) {
-                    const int gl = tg * (KS / 4) + h * (KSH / 4) + s4;
-                    const f4 c = cL[gran(gl / G, gl % G)];
+                    // granule gl = 16 tg + 8 h + sig(s4) lands at gran(gl/G, gl%G)
+                    // = 16 tg + 8 h + s4: the permutation undoes the rotation
+                    const f4 c = cL[tg * (KS / 4) + h * (KSH / 4) + s4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) lacc[u] = mfma32(c[u], kr[4 * s4 + u], lacc[u]);
                 }

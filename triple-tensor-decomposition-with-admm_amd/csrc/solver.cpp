@@ -11,17 +11,29 @@
 // several sessions on one device instead.
 #include "solver.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <sys/mman.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 namespace tritd {
 
 void emit_line(const char* line);  // api.cpp
+
+// roctx range over a scope (rocprofv3 --marker-trace shows them beside the
+// kernels).  The loop is asynchronous, so a range spans the host's enqueue
+// of its phase: which kernels belong to which ADMM statement, not GPU time.
+struct Range {
+    explicit Range(const char* name) { roctxRangePush(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range&) = delete;
+    Range& operator=(const Range&) = delete;
+};
 
 // ---------------------------------------------------------------------------
 // layout conversions (reference shapes <-> CP factor matrices)
@@ -831,8 +843,10 @@ void Session::iterate_fused(int k) {
     const int RP = g_.RP;
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
+    std::unique_ptr<Range> ph(new Range("update_A (:73-81)"));
     do_m1();
     apply_gram_A(AtA);
+    ph.reset(new Range("update_B (:83-88)"));
     if (comm_ && comm_->active()) {
         do_m2(M2);
         // M1 .. M2 above ran before the stop test of iteration k-1: they
@@ -855,6 +869,7 @@ void Session::iterate_fused(int k) {
         launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_, sb);
     }
     apply_gram_B(M2);
+    ph.reset(new Range("update_C (:90-95)"));
     mark(1);
     SideSolve sc;  // update_C's solve (:93 ridge) beside K2
     sc.P = AtA; sc.Q = BtB_.p; sc.alpha = 1e-9; sc.Ginv = GinvC_.p; sc.flags = ctrl_ + 2;
@@ -864,6 +879,7 @@ void Session::iterate_fused(int k) {
     allreduce(red2_.p, red2_count());
     apply_gram_C();
     // the next update_A's solve (B^TB, C^TC of this iteration) beside K5
+    ph.reset(new Range("fused update K5 (:38-59, :33)"));
     k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;
     k5side_.flags = ctrl_ + 2; k5side_.R = g_.R; k5side_.on = 1;
     if (comm_ && comm_->active()) {
@@ -959,6 +975,7 @@ void Session::run(int iters) {
             ev_iter_.push_back(k);
             mark(0);
         }
+        Range it_range("tritd:iteration");
         if (fused_) {
             iterate_fused(k);
         } else if (overlap_) {
