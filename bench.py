@@ -3,13 +3,14 @@
 config 4, the default) or the 2048x2048x256 r=16 fp32 workload
 (configs[4] = config 5, ``--config 5``).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|5] [--algo admm|als]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--algo admm|als]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A "step" is one ADMM iteration (triple_decomp_ADMM.m:31-66) over the whole
 tensor, device-resident.  With N > 1 ranks the tensor is sharded along
-mode 1 and the three per-iteration all-reduces run over
-RCCL (strong scaling: the problem size is fixed).  Rank 0 prints one JSON
+mode 1 and the two per-iteration all-reduces run over RCCL
+(strong scaling: the problem size is fixed).  `--gpus N` without a launcher
+starts the N rank processes itself.  Rank 0 prints one JSON
 line.  The CPU baseline is the C restatement of the MATLAB reference
 (oracle/tritd_ref.c, kind "port") timed on a bounded sample on rank 0.
 """
@@ -335,7 +336,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    ensure_built()
+    # one rank checks / rebuilds the library, the others wait for it (ranks
+    # building concurrently would race on the same objects)
+    if local_rank == 0:
+        ensure_built()
+    barrier()
     import tritd
     from tritd import synth
 

@@ -57,6 +57,24 @@ def test_als_virtual_shards(tritd, orc, name, P):
     check(orc, got, g["A"], g["B"], g["C"], g["errHist"], g["k"])
 
 
+@pytest.mark.parametrize("name,P,serial", [("als30_r3", 3, False), ("als17x16x20_r8", 2, False),
+                                           ("als30_r3", 3, True)])
+def test_als_device_set(tritd, orc, name, P, serial, monkeypatch):
+    """tritd_set_devices with one GPU repeated: one host thread per shard
+    (api.cpp run_als_group, in-process all-reduces); TRITD_SHOV=0 keeps the
+    phase-serial driver (run_als_group_serial)."""
+    if serial:
+        monkeypatch.setenv("TRITD_SHOV", "0")
+    g = load_golden(name)
+    tritd.set_devices([0] * P)
+    try:
+        got = tritd.triple_decomp_ALS(g["X"], g["r"], g["opts"], g["A0"], g["B0"], g["C0"],
+                                      return_iters=True)
+    finally:
+        tritd.set_devices([])
+    check(orc, got, g["A"], g["B"], g["C"], g["errHist"], g["k"])
+
+
 @pytest.mark.parametrize("shape,r", [((97, 80, 41), 8), ((64, 33, 50), 5), ((40, 48, 16), 1)])
 def test_als_padded_shapes(tritd, orc, synth, shape, r):
     """Shapes that are not multiples of the 16-row tiles, every padded rank."""

@@ -133,9 +133,13 @@ def test_gpu_ncvx_first_iterations_and_alias(tritd):
 
 
 @pytest.mark.gpu
-def test_gpu_ncvx_device_set(tritd):
+@pytest.mark.parametrize("serial", [False, True])
+def test_gpu_ncvx_device_set(tritd, serial, monkeypatch):
     """Mode-1 shards through tritd_set_devices (one GPU repeated): partial fit
-    sums, [M2 | A^TA] and M3 reduced between phases; O gathered per shard."""
+    sums, [M2 | A^TA] and M3 all-reduced; O gathered per shard.  Default one
+    host thread per shard; TRITD_SHOV=0 the phase-serial driver."""
+    if serial:
+        monkeypatch.setenv("TRITD_SHOV", "0")
     g = load_golden("nc30_r3")
     tritd.set_printer(lambda s: None)
     tritd.set_devices([0, 0, 0])

@@ -263,6 +263,67 @@ struct ThreadReducer {
     }
 };
 
+// Drive one session per shard of a device group, each on its own host thread
+// (shard 0 on the calling thread: a host print callback such as mexPrintf
+// stays on the host's thread), all through a communicator: RCCL
+// communicators from ncclCommInitAll for distinct devices, the in-process
+// ThreadReducer for one device repeated.  shard(p, comm) builds, runs and
+// reads back shard p and returns its TRITD_FLAG_* bits.  A shard that throws
+// aborts the others' collectives (ncclCommAbort / ThreadReducer::abort), so
+// no thread stays blocked; the first error is rethrown here.
+template <class F>
+void run_threaded(DeviceGroup& grp, F&& shard) {
+    const int P = grp.size();
+    std::unique_ptr<ThreadReducer> red;
+    if (grp.same) red.reset(new ThreadReducer(P));
+    std::vector<tritd_comm> comms((size_t)P);
+    for (int p = 0; p < P; ++p) {
+        comms[p].nranks = P;
+        comms[p].rank = p;
+        comms[p].device = grp.devs[p];
+        if (grp.same) {
+            comms[p].host_fn = &ThreadReducer::allreduce;
+            comms[p].host_user = &red->ranks[p];
+        } else {
+            comms[p].comm = g_comms[p];  // owned by the cache (group_comms)
+        }
+    }
+    std::vector<std::exception_ptr> err((size_t)P);
+    std::vector<uint32_t> fl((size_t)P, 0);
+    bool aborted_rccl = false;
+    std::mutex abort_m;
+    auto abort_all = [&] {
+        if (red) {
+            red->abort();
+            return;
+        }
+        std::lock_guard<std::mutex> lk(abort_m);
+        if (aborted_rccl) return;
+        aborted_rccl = true;
+        // unblocks the other shards' collectives; the communicators are gone
+        for (ncclComm_t c : g_comms)
+            if (c) (void)ncclCommAbort(c);
+        g_comms.clear();
+        g_comm_devs.clear();
+    };
+    auto body = [&](int p) {
+        try {
+            TRITD_HIP(hipSetDevice(grp.devs[p]));
+            fl[p] = shard(p, &comms[p]);
+        } catch (...) {
+            err[p] = std::current_exception();
+            abort_all();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int p = 1; p < P; ++p) th.emplace_back(body, p);
+    body(0);
+    for (auto& t : th) t.join();
+    for (int p = 0; p < P; ++p)
+        if (err[p]) std::rethrow_exception(err[p]);
+    for (int p = 0; p < P; ++p) g_last_flags |= fl[p];
+}
+
 // One ADMM problem sharded along mode 1 over `devs`, driven
 // the way one process per GPU drives it: each shard is a Session with a
 // communicator, stepped by its own host thread through the same schedule
@@ -303,64 +364,18 @@ void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t 
         if (iters) *iters = k;
         return;
     }
-    std::unique_ptr<ThreadReducer> red;
-    if (grp.same) red.reset(new ThreadReducer(P));
-    std::vector<tritd_comm> comms((size_t)P);
-    for (int p = 0; p < P; ++p) {
-        comms[p].nranks = P;
-        comms[p].rank = p;
-        comms[p].device = devs[p];
-        if (grp.same) {
-            comms[p].host_fn = &ThreadReducer::allreduce;
-            comms[p].host_user = &red->ranks[p];
-        } else {
-            comms[p].comm = g_comms[p];  // owned by the cache (group_comms)
-        }
-    }
-    std::vector<std::exception_ptr> err((size_t)P);
-    std::vector<uint32_t> fl((size_t)P, 0);
-    std::vector<int> kk((size_t)P, 0);
-    bool aborted_rccl = false;
-    std::mutex abort_m;
-    auto abort_all = [&] {
-        if (red) {
-            red->abort();
-            return;
-        }
-        std::lock_guard<std::mutex> lk(abort_m);
-        if (aborted_rccl) return;
-        aborted_rccl = true;
-        // unblocks the other shards' collectives; the communicators are gone
-        for (ncclComm_t c : g_comms)
-            if (c) (void)ncclCommAbort(c);
-        g_comms.clear();
-        g_comm_devs.clear();
-    };
-    auto shard = [&](int p) {
-        try {
-            const auto [i0, i1] = grp.rows(p, n1);
-            TRITD_HIP(hipSetDevice(devs[p]));
-            Session s(devs[p], static_cast<const char*>(D) + i0 * es, n1, n1, n2, n3, i0, i1, r, o,
-                      A0, B0, C0, &comms[p], flags);
-            s.run(o.maxIter);
-            s.get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr,
-                  O ? static_cast<char*>(O) + i0 * es : nullptr,
-                  E ? static_cast<char*>(E) + i0 * es : nullptr, n1, p == 0 ? errHist : nullptr,
-                  &kk[p]);
-            fl[p] = s.flags();
-        } catch (...) {
-            err[p] = std::current_exception();
-            abort_all();
-        }
-    };
-    std::vector<std::thread> th;
-    for (int p = 1; p < P; ++p) th.emplace_back(shard, p);
-    shard(0);
-    for (auto& t : th) t.join();
-    for (int p = 0; p < P; ++p)
-        if (err[p]) std::rethrow_exception(err[p]);
-    for (int p = 0; p < P; ++p) g_last_flags |= fl[p];
-    if (iters) *iters = kk[0];
+    run_threaded(grp, [&](int p, tritd_comm* comm) {
+        const auto [i0, i1] = grp.rows(p, n1);
+        Session s(devs[p], static_cast<const char*>(D) + i0 * es, n1, n1, n2, n3, i0, i1, r, o, A0,
+                  B0, C0, comm, flags);
+        s.run(o.maxIter);
+        int k = 0;
+        s.get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr,
+              O ? static_cast<char*>(O) + i0 * es : nullptr,
+              E ? static_cast<char*>(E) + i0 * es : nullptr, n1, p == 0 ? errHist : nullptr, &k);
+        if (p == 0 && iters) *iters = k;
+        return s.flags();
+    });
 }
 
 // The phase-serial schedule (TRITD_SHOV=0): every iteration runs the four
@@ -411,11 +426,47 @@ void run_group_serial(const std::vector<int>& devs, const void* D, size_t es, ui
 
 // triple_decomp_ALS over a device set: the ALS phases (als.cpp) with the
 // fit sum, [M2 | A^TA] and M3 reduced between them.
+void run_als_group_serial(const std::vector<int>& devs, const double* X, int64_t n1, int64_t n2,
+                          int64_t n3, int32_t r, int maxIter, double tol, const double* A0,
+                          const double* B0, const double* C0, double* A, double* B, double* C,
+                          double* errHist, int32_t* iters, const NcvxParams* ncvx, double* O);
+
+// triple_decomp_ALS / the test.m solver over a device set: one AlsSession
+// per shard with a communicator (its run() carries the fit-sum, [M2 | A^TA]
+// and M3 all-reduces), one host thread per shard (run_threaded);
+// TRITD_SHOV=0 keeps the phase-serial order (run_als_group_serial).
 void run_als_group(const std::vector<int>& devs, const double* X, int64_t n1, int64_t n2,
                    int64_t n3, int32_t r, int maxIter, double tol, const double* A0,
                    const double* B0, const double* C0, double* A, double* B, double* C,
                    double* errHist, int32_t* iters, const NcvxParams* ncvx = nullptr,
                    double* O = nullptr) {
+    {
+        const char* sh = std::getenv("TRITD_SHOV");
+        if (sh && std::atoi(sh) == 0) {
+            run_als_group_serial(devs, X, n1, n2, n3, r, maxIter, tol, A0, B0, C0, A, B, C, errHist,
+                                 iters, ncvx, O);
+            return;
+        }
+    }
+    DeviceGroup grp(devs, n1);
+    run_threaded(grp, [&](int p, tritd_comm* comm) {
+        const auto [i0, i1] = grp.rows(p, n1);
+        AlsSession s(devs[p], X + i0, n1, n1, n2, n3, i0, i1, r, maxIter, tol, A0, B0, C0,
+                     grp.size() > 1 ? comm : nullptr, 0);
+        if (ncvx) s.enable_ncvx(*ncvx);
+        s.run(maxIter);
+        int k = 0;
+        s.get(A, p == 0 ? B : nullptr, p == 0 ? C : nullptr, p == 0 ? errHist : nullptr, &k);
+        if (ncvx && O) s.get_O(O + s.geom().i0, n1);
+        if (p == 0 && iters) *iters = k;
+        return s.flags();
+    });
+}
+
+void run_als_group_serial(const std::vector<int>& devs, const double* X, int64_t n1, int64_t n2,
+                          int64_t n3, int32_t r, int maxIter, double tol, const double* A0,
+                          const double* B0, const double* C0, double* A, double* B, double* C,
+                          double* errHist, int32_t* iters, const NcvxParams* ncvx, double* O) {
     DeviceGroup grp(devs, n1);
     const int P = grp.size();
     std::vector<std::unique_ptr<AlsSession>> ss;
