@@ -1,10 +1,15 @@
-"""List VMEM stores whose address or data VGPRs are the destination of an
-asynchronous return (ds_read*, buffer_load*, global_load*) issued within the
-next N instructions, per kernel of a gfx950 assembly file.  A diagnostic for
-the dense-E K5 corruption: the returning write can land
-before the store has read its VGPRs.
+"""List wide VMEM stores (dwordx3/x4: more than 64 bits of data per lane)
+whose data VGPRs are rewritten within the next N instructions — by a VALU
+instruction or by an asynchronous return (ds_read*, buffer_load*,
+global_load*) — per kernel of a gfx950 assembly file.
 
-    python tools/scan_store_war.py file.s [N]
+On MI355X such a rewrite 3-4 instructions after a `buffer_store_dwordx4`
+(the compiler's hazard padding is satisfied) was measured to replace the
+store's first 64-bit word in lanes 12-15 of each 16 now and then: the
+dense-E K5 corruption of round 4.  The kernels hold the
+data of their wide stores live past a later point instead (K5_KEEP).
+
+    python tools/scan_store_war.py file.s [N] [kernel-substring]
 """
 import re
 import sys
@@ -19,38 +24,47 @@ def regs(tok):
     return {int(m.group(1))} if m else set()
 
 
-def main():
-    path = sys.argv[1]
-    N = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+def scan(lines, N, want=""):
     kern = None
-    lines = open(path).read().splitlines()
     hits = {}
     for n, l in enumerate(lines):
         mk = re.match(r"^(_Z\w+):", l)
         if mk:
             kern = mk.group(1)
-        t = l.strip()
-        if not (t.startswith("buffer_store") or t.startswith("global_store")):
+        if want and (kern is None or want not in kern):
             continue
-        ops = [x for x in t.split(None, 1)[1].split(",")]
-        if t.startswith("global_store"):
-            src = regs(ops[0]) | regs(ops[1])
-        else:
-            src = regs(ops[0]) | regs(ops[1])
-        for m in range(n + 1, min(n + 1 + N, len(lines))):
+        t = l.strip()
+        if not re.match(r"(buffer|global)_store_dwordx[34]\b", t):
+            continue
+        ops = t.split(None, 1)[1].split(",")
+        data = regs(ops[1]) if t.startswith("global_store") else regs(ops[0])
+        cnt = 0
+        for m in range(n + 1, len(lines)):
             u = lines[m].strip()
             if not u or u.startswith(";") or u.startswith("."):
                 continue
+            if u.endswith(":"):  # a label: the path forks
+                break
+            cnt += 1
+            if cnt > N:
+                break
             op = u.split(None, 1)
-            if len(op) < 2:
+            if len(op) < 2 or "store" in op[0] or op[0].startswith(("ds_write", "s_", "v_mfma")):
                 continue
-            if op[0].startswith(("ds_read", "buffer_load", "global_load", "ds_bpermute", "ds_swizzle")):
-                if regs(op[1].split(",")[0]) & src:
-                    hits.setdefault(kern, []).append((n, m - n, op[0], t[:70]))
-                    break
+            if regs(op[1].split(",")[0]) & data:
+                hits.setdefault(kern, []).append((n + 1, cnt, op[0], t[:64]))
+                break
+    return hits
+
+
+def main():
+    path = sys.argv[1]
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    want = sys.argv[3] if len(sys.argv) > 3 else ""
+    hits = scan(open(path).read().splitlines(), N, want)
     for k, v in hits.items():
         print(k, len(v))
-        for h in v[:6]:
+        for h in v:
             print("   ", h)
 
 

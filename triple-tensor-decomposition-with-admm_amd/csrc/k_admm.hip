@@ -447,6 +447,20 @@ void k5_fused(K5Args a) {
             if (pf) load_slot(tt + 2, cx);  // cx.ce and cx.cep were consumed above
         }
         double tr[4], En[4];
+        // The data of this step's wide stores (Y_L, E, T) is held live past
+        // a later point (the asm statements below), so the register
+        // allocator cannot rewrite those registers right behind the store.
+        // Round 4, measured: without it the dense-E form wrote a wrong first
+        // 8-byte word in lanes 12-15 of each 16 of a Y_L store now and then
+        // (tens of elements per launch at config 3's shape, not
+        // reproducible run to run), where the compiler placed a 64-bit VALU
+        // write of the data registers 3-4 instructions after a
+        // buffer_store_dwordx4 — the signature tools/store_hazard.hip shows
+        // for a rewrite with no wait state.  Costs no time (K5 0.934 vs
+        // 0.933 ms, profiles/round4/ab_k5_keep.txt).
+        d2v keep[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) keep[q] = d2v{0.0, 0.0};
         if constexpr (PRO) {
 #pragma unroll
             for (int p = 0; p < 2; ++p)
@@ -504,6 +518,7 @@ void k5_fused(K5Args a) {
                     tr[r] = Tn;
                 }
                 bst(YLn2, rYL, tt, p);
+                keep[p] = YLn2;
             }
             if constexpr (DE) {  // E^(k+1) over E^(k-1), densely
                 __builtin_nontemporal_store(d2v{En[0], En[1]}, Ep2 + o);
@@ -512,6 +527,8 @@ void k5_fused(K5Args a) {
             } else if (!K5_ORD) {
                 ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
             }
+            keep[2] = d2v{En[0], En[1]};
+            keep[3] = d2v{En[2], En[3]};
         }
         // T -> "TX" order (common.h): lane l, slot s holds T(ij = 4s+(l>>4), t = l&15)
 #pragma unroll
@@ -524,7 +541,10 @@ void k5_fused(K5Args a) {
             tv[0] = ts[il * 17 + 4 * (2 * p) + tg];
             tv[1] = ts[il * 17 + 4 * (2 * p + 1) + tg];
             bst(tv, rT, tt, p);
+            keep[4 + p] = tv;
         }
+        // Y_L and E data live until here (past the T transpose and stores)
+        asm volatile("" ::"v"(keep[0]), "v"(keep[1]), "v"(keep[2]), "v"(keep[3]));
         // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4);
         // the C/D register of T is directly the B operand
 #pragma unroll
@@ -535,6 +555,8 @@ void k5_fused(K5Args a) {
         // (K5_ORD: the encode's LDS round trips after the W MFMAs, its rare
         // dense-store branch last)
         if constexpr (K5_ORD && !PRO && !DE) ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
+        // T data live until here (past the W MFMAs)
+        asm volatile("" ::"v"(keep[4]), "v"(keep[5]));
         // the slice SD t-tiles ahead into the buffer read SD t-tiles ago
         if (ps) stage_store(slice_buf(tt + SD - t0));
         if (bar) __syncthreads();
