@@ -30,5 +30,6 @@ find $O/stats $O/prims_stats -name "*kernel_stats.csv" | head -3
 if [ -n "${SMALL:-}" ]; then
   timeout -k 10 300 python3 bench.py --config 2 --no-e2e --no-prims > profiles/round4/c2_bench_line.json 2> $O/c2.err || exit $?
   timeout -k 10 300 python3 bench.py --config 3 --no-e2e --no-prims > profiles/round4/c3_bench_line.json 2> $O/c3.err || exit $?
-  cut -c1-200 profiles/round4/c2_bench_line.json profiles/round4/c3_bench_line.json
+  timeout -k 10 400 python3 bench.py --config 5 --no-e2e --no-prims --no-cpu > profiles/round4/c5_bench_line.json 2> $O/c5.err || exit $?
+  cut -c1-200 profiles/round4/c2_bench_line.json profiles/round4/c3_bench_line.json profiles/round4/c5_bench_line.json
 fi
