@@ -48,6 +48,7 @@
 // same k, including a near-tolerance stop golden).  The norm sums of :59 use
 // FMAs too: their summation order is this kernel's own (per lane, then a
 // fixed-order tree), never MATLAB's.
+#include "finish.h"
 #include "kernels.h"
 #include "sweep.h"
 #include "wtrace.h"
@@ -757,27 +758,6 @@ void launch_reduce_pairs(const double* partial, int n, double* out, const int* s
     TRITD_CHECK_LAUNCH();
 }
 
-// ctrl[0] = stop flag, ctrl[1] = iterations completed (k of :68)
-__device__ __forceinline__ void finish_body(const double* ss, double normD, int k, double tol,
-                                            double* errHist, double* errL, double* errO, int* ctrl,
-                                            int single) {
-    double eL = sqrt(ss[0]) / normD;  // norm(resL(:))/normD
-    double eO = sqrt(ss[1]) / normD;  // norm(resO(:))/normD
-    double e = eL + eO;               // :59
-    if (single) {  // single residuals: single norms, single quotients and sum
-        const float fL = (float)sqrt(ss[0]) / (float)normD;
-        const float fO = (float)sqrt(ss[1]) / (float)normD;
-        eL = fL;
-        eO = fO;
-        e = (double)(fL + fO);
-    }
-    errHist[k - 1] = e;
-    errL[k - 1] = eL;
-    errO[k - 1] = eO;
-    ctrl[1] = k;
-    if (k > 1 && fabs(e - errHist[k - 2]) < tol * errHist[k - 2]) ctrl[0] = 1;  // :63
-}
-
 __global__ void k_finish(const double* ss, double normD, int k, double tol, double* errHist,
                          double* errL, double* errO, int* ctrl, int single) {
     if (ctrl[0]) return;
@@ -788,44 +768,16 @@ __global__ void k_finish(const double* ss, double normD, int k, double tol, doub
 // read).  The sharded schedule's norm partials live in red1_'s tail, sized to
 // the largest shard's K5 grid; a rank with fewer workgroups leaves the slots
 // past its own at zero, and the all-reduce writes sums into all of them.
-__global__ __launch_bounds__(256) void k_reduce_finish(double* __restrict__ p, int n,
-                                                       double normD, int k, double tol,
-                                                       double* errHist, double* errL, double* errO,
-                                                       int* ctrl, int single, int clear) {
-    if (ctrl[0]) return;
-    __shared__ double sx[256], sy[256];
-    double x = 0.0, y = 0.0;
-#pragma unroll 8  // loads batched; the sums keep their sequential order
-    for (int b = threadIdx.x; b < n; b += 256) {
-        x += p[2 * b];
-        y += p[2 * b + 1];
-    }
-    if (clear)
-        for (int b = threadIdx.x; b < n; b += 256) {
-            p[2 * b] = 0.0;
-            p[2 * b + 1] = 0.0;
-        }
-    sx[threadIdx.x] = x;
-    sy[threadIdx.x] = y;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-            sx[threadIdx.x] += sx[threadIdx.x + w];
-            sy[threadIdx.x] += sy[threadIdx.x + w];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const double ss[2] = {sx[0], sy[0]};
-        finish_body(ss, normD, k, tol, errHist, errL, errO, ctrl, single);
-    }
-}
+__global__ __launch_bounds__(256) void k_reduce_finish(FinishArgs f) { reduce_finish_wg<256>(f); }
 
 void launch_reduce_finish(double* partial, int n, double normD, int k, double tol,
                           double* errHist, double* errL, double* errO, int* ctrl, bool single,
                           hipStream_t st, bool clear) {
-    hipLaunchKernelGGL(k_reduce_finish, dim3(1), dim3(256), 0, st, partial, n, normD, k, tol,
-                       errHist, errL, errO, ctrl, (int)single, (int)clear);
+    FinishArgs f;
+    f.p = partial; f.n = n; f.normD = normD; f.k = k; f.tol = tol;
+    f.errHist = errHist; f.errL = errL; f.errO = errO; f.ctrl = ctrl;
+    f.single = (int)single; f.clear = (int)clear; f.on = 1;
+    hipLaunchKernelGGL(k_reduce_finish, dim3(1), dim3(256), 0, st, f);
     TRITD_CHECK_LAUNCH();
 }
 

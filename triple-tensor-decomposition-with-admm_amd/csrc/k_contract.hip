@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <utility>
 
+#include "finish.h"
 #include "kernels.h"
 #include "sweep.h"
 #include "wtrace.h"
@@ -45,7 +46,16 @@ template <int M1_WAVES, bool SETS>
 __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__ Wk,
                                                       const double* __restrict__ Bh, double* M1,
                                                       int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                                      const int* stop, int sets, int64_t sstride) {
+                                                      const int* stop, int sets, int64_t sstride,
+                                                      FinishArgs fin) {
+    // the extra column of workgroups: the previous iteration's norm
+    // reduction and stop test in its first one (the others exit).  The
+    // contraction below may run before or after it: it writes only M1 (the
+    // stop flag gates the kernels that follow)
+    if (fin.on && blockIdx.x == gridDim.x - 1) {
+        if (blockIdx.y == 0) reduce_finish_wg<64 * M1_WAVES>(fin);
+        return;
+    }
     if (*stop) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * 64 + lane;
@@ -82,16 +92,16 @@ __global__ __launch_bounds__(64 * M1_WAVES) void k_m1(const double* __restrict__
 }
 
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
-               hipStream_t st) {
+               hipStream_t st, const FinishArgs& fin) {
     // 4 slices when the row blocks alone fill the chip (512 rows: 36 vs 39 us
     // with 16), 16 for short shards (64 rows: 64 blocks)
     // (16-byte-load variants, two rows per lane, measured neutral or slower
     // in the solver: DESIGN.md §4)
-    const dim3 grid((unsigned)cdiv(g.n1p, 64), g.RP);
+    const dim3 grid((unsigned)cdiv(g.n1p, 64) + (fin.on ? 1 : 0), g.RP);
     const int sets = g.tsplit;
     const int64_t ss = (int64_t)g.RP * g.plane;
 #define M1_LAUNCH(NW, S) \
-    hipLaunchKernelGGL((k_m1<NW, S>), grid, dim3(64 * NW), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop, sets, ss)
+    hipLaunchKernelGGL((k_m1<NW, S>), grid, dim3(64 * NW), 0, st, Wk, Bh, M1, g.n1p, g.n2, g.plane, g.RP, stop, sets, ss, fin)
     if (g.n1p >= 256) {  // (two rows per lane with 16-B loads halves the waves: 72 vs 36 us)
         if (sets > 1) M1_LAUNCH(4, true); else M1_LAUNCH(4, false);
     } else {

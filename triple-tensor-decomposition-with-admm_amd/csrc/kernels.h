@@ -27,6 +27,24 @@ struct SideSolve {
     int on = 0;
 };
 
+// The reduction + stop test of one iteration's K5 norm pairs, run by an
+// extra workgroup of the next iteration's M1 (single GPU: one launch less per
+// iteration; finish.h)
+struct FinishArgs {
+    double* p = nullptr;  // n [sum resL^2, sum resO^2] pairs
+    int n = 0;
+    double normD = 0.0;
+    int k = 0;
+    double tol = 0.0;
+    double* errHist = nullptr;
+    double* errL = nullptr;
+    double* errO = nullptr;
+    int* ctrl = nullptr;
+    int single = 0;
+    int clear = 0;
+    int on = 0;
+};
+
 struct K5Args {
     const double* D;
     double* O;
@@ -83,8 +101,10 @@ void launch_finish(const double* ss, double normD, int k, double tol, double* er
                    double* errO, int* ctrl, bool single, hipStream_t st);
 
 // ---- contractions and small linear algebra (k_contract.hip) ---------------
+// fin.on: the previous iteration's norm reduction and stop test in an extra
+// workgroup (finish.h)
 void launch_m1(const Geom& g, const double* Wk, const double* Bh, double* M1, const int* stop,
-               hipStream_t st);
+               hipStream_t st, const FinishArgs& fin = FinishArgs{});
 // side: update_B's R x R solve in an extra workgroup (RP <= 64)
 void launch_m2(const Geom& g, const double* Wk, const double* AhT, double* M2, const int* stop,
                hipStream_t st, const SideSolve& side = SideSolve{});

@@ -376,8 +376,18 @@ void Session::do_m1() {
         launch_m1_qi(g_, g_.r, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
     else if (f32_)
         launch_m1_32(g_, Wk_.f(), Bh_.p, M1_.f(), ctrl_, st_);
-    else
-        launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
+    else {
+        // single GPU, fused schedule: the previous K5's norm reduction and
+        // stop test ride in an extra workgroup of this M1 (finish.h)
+        FinishArgs f;
+        if (norms_pending_ && !(comm_ && comm_->active())) {
+            f.p = k5part_.p; f.n = k5n(); f.normD = normD_; f.k = pend_k_; f.tol = o_.tol;
+            f.errHist = errHist_.p; f.errL = errL_.p; f.errO = errO_.p; f.ctrl = ctrl_;
+            f.single = (int)f32_; f.on = 1;
+            norms_pending_ = false;
+        }
+        launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_, f);
+    }
 }
 
 void Session::do_m2(double* M2) {
@@ -639,6 +649,12 @@ void Session::set_ah(int k) {
 
 void Session::flush_norms() {
     if (!norms_pending_) return;
+    if (!(comm_ && comm_->active())) {  // single GPU: K5's own partials
+        launch_reduce_finish(k5part_.p, k5n(), normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
+                             ctrl_, f32_, st_);
+        norms_pending_ = false;
+        return;
+    }
     double* parts = red1_.p + red1_count();
     allreduce(parts, 2 * (int64_t)k5tail_);
     launch_reduce_finish(parts, k5tail_, normD_, pend_k_, o_.tol, errHist_.p, errL_.p, errO_.p,
@@ -893,7 +909,13 @@ void Session::iterate_fused(int k) {
         norms_pending_ = true;
         pend_k_ = k;
     } else {
-        launch_k5_full(k, /*fused_finish=*/true);
+        // the norm reduction and stop test of k ride in the next M1 (do_m1),
+        // or flush_norms when the loop ends first
+        mark(3);
+        launch_k5_any(k, /*prologue=*/false);
+        mark(4);
+        norms_pending_ = true;
+        pend_k_ = k;
     }
 }
 
