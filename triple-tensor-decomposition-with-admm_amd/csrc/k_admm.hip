@@ -653,12 +653,14 @@ int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }
 
 // t-split of the fp64 K5 walk: a problem with few ij-tiles (the sensor shape
 // 54x4x1152: 16 ij-tiles, 4 workgroups walking 72 t-tiles each) leaves the GPU
-// almost idle, so the walk is cut into chunks of >= 8 t-tiles until there are
-// about 256 workgroups; each chunk's W is a partial sum (k_w_reduce).
+// almost idle, so the walk is cut into chunks of >= 4 t-tiles until there are
+// about 256 workgroups; each chunk's W is a partial set that M1 / M2 sum as
+// they read W.  (Config 2, round 4: 18 chunks of 4 against 9 of 8, iteration
+// 0.106 vs 0.114 ms; 36 of 2: 0.113 ms — tools/round4_c2_tsplit.sh.)
 int k5_tsplit(const Geom& g) {
     if (g.RP > 64) return 1;
     const int64_t wg = cdiv(g.tiles, K5_WAVES);
-    const int64_t smax = g.ntt / 8 > 1 ? g.ntt / 8 : 1;  // chunks of >= 8 t-tiles
+    const int64_t smax = g.ntt / 4 > 1 ? g.ntt / 4 : 1;  // chunks of >= 4 t-tiles
     if (const char* e = std::getenv("TRITD_K5_TSPLIT")) {  // override (read once per session)
         const int64_t f = std::atoll(e);
         return (int)(f < 1 ? 1 : (f > g.ntt ? g.ntt : f));
