@@ -25,6 +25,14 @@ struct SideSolve {
     int* flags = nullptr;
     int R = 0;
     int on = 0;
+    // gram_rows > 0: the side workgroup first forms one operand itself,
+    // gram_to = X^T X of the row-major [gram_rows][RP] factor gram_src, which
+    // then stands for P (gram_which = 0) or Q (1): the fused single-GPU
+    // schedule's Grams ride in the side job instead of a launch of their own
+    const double* gram_src = nullptr;
+    double* gram_to = nullptr;
+    int64_t gram_rows = 0;
+    int gram_which = 0;
 };
 
 // The reduction + stop test of one iteration's K5 norm pairs, run by an

@@ -466,32 +466,67 @@ bool Session::small_ag(int64_t rows) const {
     return !f32_ && !qi_ && g_.RP <= 64 && apply_gram_small(g_.RP, rows);
 }
 
-void Session::apply_gram_A(double* AtA) {
+// Small factors (rows*RP^2 <= 327 680): with defer (the fused single-GPU
+// schedule, side_gram_ok) the apply alone, the Gram left to the side solve
+// that next reads it (SideSolve::gram_rows), else apply + Gram in one
+// single-workgroup launch.  Larger factors: an apply and a Gram launch (a
+// side-job Gram of 512 x 64 outlasts M2: config 4 1.34 -> 1.41 ms).
+// Returns whether the Gram was left to the side solve.
+bool Session::apply_gram_A(double* AtA, bool defer) {
+    if (defer && small_ag(g_.n1p)) {
+        do_apply_A(GinvA_.p);
+        return true;
+    }
     if (small_ag(g_.n1p)) {
         launch_apply_gram(g_.RP, M1_.p, g_.n1p, GinvA_.p, Ah_.p, AhT_.p, g_.n1p, AtA, ctrl_, ctrl_ + 2, st_);
-        return;
+        return false;
     }
     do_apply_A(GinvA_.p);
     launch_gram(g_.RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
+    return false;
 }
 
-void Session::apply_gram_B(const double* M2) {
+bool Session::apply_gram_B(const double* M2, bool defer) {
+    if (defer && small_ag(g_.n2)) {
+        do_apply_B(M2, GinvB_.p);
+        return true;
+    }
     if (small_ag(g_.n2)) {
         launch_apply_gram(g_.RP, M2, g_.n2, GinvB_.p, Bh_.p, nullptr, 0, BtB_.p, ctrl_, ctrl_ + 2, st_);
-        return;
+        return false;
     }
     do_apply_B(M2, GinvB_.p);
     launch_gram(g_.RP, Bh_.p, g_.n2, BtB_.p, ctrl_, st_);
+    return false;
 }
 
-void Session::apply_gram_C() {
+bool Session::apply_gram_C(bool defer) {
+    if (defer && small_ag(g_.n3p)) {
+        do_apply_C(GinvC_.p);
+        return true;
+    }
     if (small_ag(g_.n3p)) {
         launch_apply_gram(g_.RP, red2_.p, g_.n3p, GinvC_.p, Ch_.p, ChT_.p, g_.n3p, CtC_.p, ctrl_, ctrl_ + 2,
                           st_);
-        return;
+        return false;
     }
     do_apply_C(GinvC_.p);
     launch_gram(g_.RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, st_);
+    return false;
+}
+
+// the Grams can ride in side solves on the fused schedule with one GPU (with
+// a communicator A^TA is all-reduced with M2 before update_B's solve)
+bool Session::side_gram_ok() const {
+    return !f32_ && !qi_ && g_.RP <= 64 && !(comm_ && comm_->active());
+}
+
+// side solve `s` first forms operand `which` (0 = P, 1 = Q) as X^T X into `to`
+static void with_gram(SideSolve& s, const double* X, int64_t rows, double* to, int which) {
+    s.gram_src = X;
+    s.gram_rows = rows;
+    s.gram_to = to;
+    s.gram_which = which;
 }
 
 void Session::launch_k5_any(int k, bool prologue) {
@@ -860,8 +895,9 @@ void Session::iterate_fused(int k) {
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
     std::unique_ptr<Range> ph(new Range("update_A (:73-81)"));
+    const bool defer = side_gram_ok();
     do_m1();
-    apply_gram_A(AtA);
+    const bool gA = apply_gram_A(AtA, defer);
     ph.reset(new Range("update_B (:83-88)"));
     if (comm_ && comm_->active()) {
         do_m2(M2);
@@ -882,22 +918,25 @@ void Session::iterate_fused(int k) {
         SideSolve sb;
         sb.P = AtA; sb.Q = CtC_.p; sb.alpha = o_.lambda2; sb.Ginv = GinvB_.p; sb.flags = ctrl_ + 2;
         sb.R = g_.R; sb.on = 1;
+        if (gA) with_gram(sb, Ah_.p, g_.n1p, AtA, 0);
         launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_, sb);
     }
-    apply_gram_B(M2);
+    const bool gB = apply_gram_B(M2, defer);
     ph.reset(new Range("update_C (:90-95)"));
     mark(1);
     SideSolve sc;  // update_C's solve (:93 ridge) beside K2
     sc.P = AtA; sc.Q = BtB_.p; sc.alpha = 1e-9; sc.Ginv = GinvC_.p; sc.flags = ctrl_ + 2;
     sc.R = g_.R; sc.on = 1;
+    if (gB) with_gram(sc, Bh_.p, g_.n2, BtB_.p, 1);
     launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_, 0, -1, sc);
     mark(2);
     allreduce(red2_.p, red2_count());
-    apply_gram_C();
+    const bool gC = apply_gram_C(defer);
     // the next update_A's solve (B^TB, C^TC of this iteration) beside K5
     ph.reset(new Range("fused update K5 (:38-59, :33)"));
     k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;
     k5side_.flags = ctrl_ + 2; k5side_.R = g_.R; k5side_.on = 1;
+    if (gC) with_gram(k5side_, Ch_.p, g_.n3p, CtC_.p, 1);
     if (comm_ && comm_->active()) {
         // the norm partials stay per workgroup in red1_'s tail: all-reduced
         // with the next iteration's M2 | A^TA (or by flush_norms)

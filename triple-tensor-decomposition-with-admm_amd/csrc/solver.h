@@ -142,9 +142,10 @@ class Session {
     void create_streams(hipStream_t shared_stream);
     void launch_k5_full(int k, bool fused_finish);
     bool small_ag(int64_t rows) const;
-    void apply_gram_A(double* AtA);
-    void apply_gram_B(const double* M2);
-    void apply_gram_C();
+    bool apply_gram_A(double* AtA, bool defer = false);
+    bool apply_gram_B(const double* M2, bool defer = false);
+    bool apply_gram_C(bool defer = false);
+    bool side_gram_ok() const;
     bool overlap_ = false;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;

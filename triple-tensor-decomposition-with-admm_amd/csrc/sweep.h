@@ -61,6 +61,40 @@ __device__ __forceinline__ void sweep_all(double (&a)[RW], double* rowbuf, doubl
 // Ginv is written directly (R x R block, zero pad), with the pinv request of
 // pinv.h (the consumer replaces the inverse by pinv when the pivots come near
 // MATLAB's cutoff).
+// G = X^T X (RP x RP) of a row-major [rows][RP] factor in one workgroup of
+// NW waves: wave w takes the 16 x 16 tiles w, w + NW, ... of G, each over all
+// K-steps of 4 rows on v_mfma_f64_16x16x4_f64 (A[m][k] = X(i+k, 16ta+m),
+// B[k][n] = X(i+k, 16tb+n)), loads 8 K-steps ahead; rows past the end are zero
+template <int RP, int NW>
+__device__ __forceinline__ void side_gram(const double* __restrict__ X, int64_t rows, double* G) {
+    typedef double g4 __attribute__((ext_vector_type(4)));
+    constexpr int NT = RP / 16, U = 8;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m = lane & 15, kq = lane >> 4;
+    const int64_t steps = (rows + 3) >> 2;
+    for (int t = w; t < NT * NT; t += NW) {
+        const int ta = t / NT, tb = t - (t / NT) * NT;
+        const double* xa = X + 16 * ta + m;
+        const double* xb = X + 16 * tb + m;
+        g4 acc = g4{0.0, 0.0, 0.0, 0.0};
+        for (int64_t s0 = 0; s0 < steps; s0 += U) {
+            double a[U], b[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = 4 * (s0 + u) + kq;
+                const bool in = i < rows;
+                a[u] = in ? xa[i * RP] : 0.0;
+                b[u] = in ? xb[i * RP] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+        }
+        // C/D element r of lane l: G(16ta + (l>>4) + 4r, 16tb + (l&15))
+#pragma unroll
+        for (int r = 0; r < 4; ++r) G[(int64_t)(16 * ta + kq + 4 * r) * RP + 16 * tb + m] = acc[r];
+    }
+}
+
 template <int RP, int NW = 4>
 __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, double* pivs) {
     // the host kernel's other workgroups share this CU's SIMDs: win issue
@@ -68,12 +102,22 @@ __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, d
     constexpr int RW = RP / NW;
     const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int cc = c < RP ? c : 0;  // lanes >= RP read a valid column, never written back
+    const double* P = s.P;
+    const double* Q = s.Q;
+    if (s.gram_rows > 0) {
+        side_gram<RP, NW>(s.gram_src, s.gram_rows, s.gram_to);
+        __syncthreads();  // (workgroup scope: the Gram is read back below by other waves)
+        if (s.gram_which == 0)
+            P = s.gram_to;
+        else
+            Q = s.gram_to;
+    }
     double a[RW];
 #pragma unroll
     for (int q = 0; q < RW; ++q) {
         const int i = RW * w + q;
         const bool in = (i < s.R) && (c < s.R);
-        const double pq = s.P[i * RP + cc] * s.Q[i * RP + cc];
+        const double pq = P[i * RP + cc] * Q[i * RP + cc];
         const double g = (i == c) ? pq + s.alpha : pq;
         a[q] = in ? g : ((i == c) ? 1.0 : 0.0);
     }
@@ -87,7 +131,7 @@ __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, d
             s.Ginv[i * RP + c] = (i < s.R && c < s.R) ? -a[q] : 0.0;
         }
     // pinv's cutoff near: save the Gram and request the fallback (pinv.h)
-    pinv_request<64 * NW>(pivots_near_cutoff(pivs, s.R), s.P, s.Q, s.R, RP, s.alpha, s.Ginv);
+    pinv_request<64 * NW>(pivots_near_cutoff(pivs, s.R), P, Q, s.R, RP, s.alpha, s.Ginv);
 }
 
 }  // namespace tritd
