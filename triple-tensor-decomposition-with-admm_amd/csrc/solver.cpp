@@ -863,8 +863,20 @@ void Session::iterate_overlapped(int k) {
     TRITD_HIP(hipStreamWaitEvent(st_, evSA_, 0));
     do_apply_A(GinvA_.p);
     launch_gram(RP, Ah_.p, g_.n1p, AtA, ctrl_, st_);
-    solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
-    do_m2(M2);
+    if (RP >= 128) {
+        // padded ranks 128 / 256 (config 5): solve B (~0.15 ms, k_solve_mw)
+        // on the high-priority side stream, issued before M2 (~0.65 ms there)
+        // so that its workgroups are dispatched first and run beside it
+        TRITD_HIP(hipEventRecord(evAtA_, st_));
+        TRITD_HIP(hipStreamWaitEvent(side_, evAtA_, 0));
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, side_);
+        TRITD_HIP(hipEventRecord(evSB_, side_));
+        do_m2(M2);
+        TRITD_HIP(hipStreamWaitEvent(st_, evSB_, 0));
+    } else {
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+        do_m2(M2);
+    }
     do_apply_B(M2, GinvB_.p);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
