@@ -20,6 +20,8 @@ python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/k5_traffic.json $ALG "
 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     --output-format csv -d $O/pmc_sq -o run -- $B > $O/pmc_sq.log 2>&1 || exit $?
 python3 tools/pmc_summary.py --json $O/k2_mfma_util.json $O/pmc_sq "k_m3_cp" "k5_fused<64, false" > $O/mfma_util.txt || exit $?
+# the bench line below cites the newest profiles/round*/ PMC files: this run's
+mkdir -p profiles/round4 && cp $O/k5_traffic.json $O/k2_mfma_util.json profiles/round4/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
     python3 bench.py --no-cpu --no-e2e --no-prims > $O/stats.log 2>&1 || exit $?
 timeout -k 10 500 python3 bench.py > $O/bench_line.json 2> $O/bench.err || exit $?
