@@ -14,7 +14,8 @@
  *  - All host arrays are MATLAB column-major: X(i,j,t) at i + n1*(j + n2*t).
  *  - Factors use the reference shapes: A (n1,r,r), B (r,n2,r), C (r,r,n3).
  *  - Functions named tritd_dev_* take DEVICE pointers and a hipStream_t
- *    (passed as void*, NULL = default stream) and do not synchronise.
+ *    (passed as void*, NULL = default stream) and do not synchronise, except
+ *    the metric forms, which return host scalars (evaluate, quality).
  *  - Every function returns a tritd_status; on error the message is available
  *    from tritd_last_error() (thread-local).
  *  - Inputs are never written (MATLAB shares mxArrays copy-on-write).

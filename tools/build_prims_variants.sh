@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build libtritd variants that differ only in the -D flags of k_prims.hip, into ab/<name>.so
+#   bash tools/build_prims_variants.sh name1="-DTP_NBUF=2" ...
+set -e
+cd "$(dirname "$0")/../triple-tensor-decomposition-with-admm_amd/csrc"
+make -j8 >/dev/null
+mkdir -p ../../ab
+for spec in "$@"; do
+  name=${spec%%=*}; flags=${spec#*=}
+  rm -rf build_$name; cp -r build build_$name; rm -f build_$name/k_prims.o
+  make OBJDIR=build_$name OUT=../../ab/$name.so EXTRA="$flags" >/dev/null &
+done
+wait
+cp ../tritd/libtritd.so ../../ab/base.so
+ls -la ../../ab

@@ -3,15 +3,18 @@
 // mode, >3-D data), converts exceptions into tritd_status + a thread-local
 // message, and never writes its inputs.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "als.h"
@@ -112,6 +115,54 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 std::vector<int> g_devices;
 std::vector<int> g_comm_devs;
 std::vector<ncclComm_t> g_comms;
+
+// Scratch of the device-form products (packed factor copies), kept per
+// (device, stream) and grown on demand, so that a call returns without
+// waiting for its kernels (tritd.h: device forms do not synchronise): calls on
+// one stream are ordered by it and reuse its buffers.  Heap-held and never
+// destroyed at exit (the HIP runtime may be gone by then); tritd_shutdown
+// frees it.  (Stream-ordered hipMallocAsync scratch on the null stream read
+// back as zeros on a repeated call on ROCm 7.2: tools/iso_tp.sh, round 4.)
+// The entry's `done` event marks the end of the last call's kernels: a call
+// waits on it (device side) before overwriting the buffers, which orders it
+// after that call even when a destroyed stream's handle is reused.
+struct ScratchSet {
+    std::array<DBuf, 5> buf;
+    hipEvent_t done = nullptr;
+    ~ScratchSet() {
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+std::mutex g_scratch_mutex;
+std::map<std::pair<int, hipStream_t>, ScratchSet>* g_scratch = nullptr;
+
+// the caller holds g_scratch_mutex over the whole enqueue (two host threads
+// on one stream would otherwise interleave their packs and products)
+ScratchSet& scratch_set(hipStream_t st) {
+    if (!g_scratch) g_scratch = new std::map<std::pair<int, hipStream_t>, ScratchSet>();
+    int dev = 0;
+    TRITD_HIP(hipGetDevice(&dev));
+    ScratchSet& s = (*g_scratch)[{dev, st}];
+    if (!s.done) TRITD_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    else TRITD_HIP(hipStreamWaitEvent(st, s.done, 0));
+    return s;
+}
+
+double* scratch(ScratchSet& s, int slot, size_t count) {
+    DBuf& b = s.buf[slot];
+    if (b.p && b.n < count) {
+        TRITD_HIP(hipEventSynchronize(s.done));  // the last call may still read it
+        TRITD_HIP(hipFree(b.p));
+        b.p = nullptr;
+    }
+    if (!b.p) b.alloc(count);
+    return b.p;
+}
+
+void drop_scratch() {
+    std::lock_guard<std::mutex> lk(g_scratch_mutex);
+    if (g_scratch) g_scratch->clear();
+}
 
 void drop_comms() {
     for (ncclComm_t c : g_comms)
@@ -872,6 +923,7 @@ void tritd_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mutex);
     drop_comms();
     g_devices.clear();
+    drop_scratch();
 }
 
 // ---------------------------------------------------------------------------
@@ -1044,13 +1096,14 @@ tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, cons
         hipStream_t st = as_stream(stream);
         Geom g = make_geom(n1, n2, n3, 0, n1, r);
         g.RP = padded_rank32(g.R);  // 16..256: the kernel is instantiated for every padded rank
-        DBuf Ah, Bh, ChT;
-        Ah.alloc((size_t)(g.n1p * g.RP));
-        Bh.alloc((size_t)(n2 * g.RP));
-        ChT.alloc((size_t)g.RP * g.n3p);
-        launch_pack_factors(g, A, B, C, Ah.p, Bh.p, ChT.p, st);
-        launch_tp(g, Ah.p, Bh.p, ChT.p, X, nullptr, nullptr, 0, n1, n1 * n2, st);
-        TRITD_HIP(hipStreamSynchronize(st));  // the factor copies are freed on return
+        std::lock_guard<std::mutex> lk(g_scratch_mutex);
+        ScratchSet& ss = scratch_set(st);
+        double* Ah = scratch(ss, 0, (size_t)(g.n1p * g.RP));
+        double* Bh = scratch(ss, 1, (size_t)(n2 * g.RP));
+        double* ChT = scratch(ss, 2, (size_t)g.RP * g.n3p);
+        launch_pack_factors(g, A, B, C, Ah, Bh, ChT, st);
+        launch_tp(g, Ah, Bh, ChT, X, nullptr, nullptr, 0, n1, n1 * n2, st);
+        TRITD_HIP(hipEventRecord(ss.done, st));
     });
 }
 
@@ -1064,17 +1117,18 @@ tritd_status tritd_dev_triple_product_qi_f64(const double* A, const double* B, c
         hipStream_t st = as_stream(stream);
         Geom g = make_geom(n1, n2, n3, 0, n1, r);
         g.RP = padded_rank32(g.R);
-        DBuf Ah, Bh, ChT, H, ones;
-        Ah.alloc((size_t)(g.n1p * g.RP));
-        Bh.alloc((size_t)(n2 * g.RP));
-        ChT.alloc((size_t)g.RP * g.n3p);
-        H.alloc((size_t)(g.n1p * n2 * g.RP));
-        ones.alloc((size_t)g.RP);
-        launch_pack_factors(g, A, B, C, Ah.p, Bh.p, ChT.p, st);
-        launch_fill(ones.p, g.RP, 1.0, st);
-        launch_qi_h(g, r, Ah.p, Bh.p, H.p, nullptr, st);
-        launch_tp(g, H.p, ones.p, ChT.p, X, nullptr, nullptr, 0, n1, n1 * n2, st, g.n1p * g.RP, 0);
-        TRITD_HIP(hipStreamSynchronize(st));
+        std::lock_guard<std::mutex> lk(g_scratch_mutex);
+        ScratchSet& ss = scratch_set(st);
+        double* Ah = scratch(ss, 0, (size_t)(g.n1p * g.RP));
+        double* Bh = scratch(ss, 1, (size_t)(n2 * g.RP));
+        double* ChT = scratch(ss, 2, (size_t)g.RP * g.n3p);
+        double* H = scratch(ss, 3, (size_t)(g.n1p * n2 * g.RP));
+        double* ones = scratch(ss, 4, (size_t)g.RP);
+        launch_pack_factors(g, A, B, C, Ah, Bh, ChT, st);
+        launch_fill(ones, g.RP, 1.0, st);
+        launch_qi_h(g, r, Ah, Bh, H, nullptr, st);
+        launch_tp(g, H, ones, ChT, X, nullptr, nullptr, 0, n1, n1 * n2, st, g.n1p * g.RP, 0);
+        TRITD_HIP(hipEventRecord(ss.done, st));
     });
 }
 

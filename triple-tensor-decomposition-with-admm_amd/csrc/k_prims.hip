@@ -61,7 +61,16 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 // the staging.  (Round 3's form staged 32 t-values per step without double
 // buffering, two barriers each: 0.464 ms at 512^3 r = 8, 0.47 of the MFMA peak.)
 // ---------------------------------------------------------------------------
-constexpr int TP_WAVES = 4;
+#ifndef TP_WV
+#define TP_WV 4
+#endif
+constexpr int TP_WAVES = TP_WV;
+#ifndef TP_NBUF
+#define TP_NBUF 2
+#endif
+#ifndef TP_CHAINS
+#define TP_CHAINS 1
+#endif
 
 template <int RP, int MODE>
 __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__ Ah,
@@ -76,7 +85,10 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
     constexpr int NT = 64 * TP_WAVES;
     constexpr int SP = RP * 8;  // d2v pairs per slice (RP rows of 16 t)
     constexpr int NS = (SP + NT - 1) / NT;
-    __shared__ double sct[2][RP * SK];
+    // four slice buffers staged two t-tiles ahead: a barrier after every
+    // second t-tile only (K5's scheme, k_admm.hip)
+    constexpr int NBUF = TP_NBUF, SD = NBUF / 2;  // slices staged SD t-tiles ahead
+    __shared__ double sct[NBUF][RP * SK];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int il = lane & 15, tg = lane >> 4;
     const int64_t tile = (int64_t)blockIdx.x * TP_WAVES + wid;
@@ -116,18 +128,31 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
     };
     const int64_t obase = i + ldj * j;
     double sn = 0.0, sd = 0.0;
-    stage_load(0);
-    stage_store(0);
+    for (int q = 0; q < SD; ++q)
+        if (q < ntt) {
+            stage_load(q);
+            stage_store(q);
+        }
     __syncthreads();
     for (int64_t tt = 0; tt < ntt; ++tt) {
-        const int buf = (int)(tt & 1);
-        const bool more = tt + 1 < ntt;
-        if (more) stage_load(tt + 1);
+        const int buf = (int)(tt % NBUF);
+        const bool more = tt + SD < ntt;
+        if (more) stage_load(tt + SD);
         const double* cT = sct[buf];
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        // two accumulation chains (even / odd K-steps), summed once
+        d4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+        if (TP_CHAINS == 2) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
+            for (int s = 0; s < KS; s += 2) {
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + 4 + tg) * SK + il], kr[s + 1], acc1, 0, 0, 0);
+            }
+            acc += acc1;
+        } else {
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
+        }
         // C/D element r of lane l: L(i, j, t = 16 tt + (l>>4) + 4r)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -143,8 +168,10 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
                 sd = fma(x, x, sd);
             }
         }
-        if (more) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
-        __syncthreads();
+        // the slice two t-tiles ahead into the buffer read two t-tiles ago;
+        // one of any two consecutive steps ends at the barrier
+        if (more) stage_store((int)((tt + SD) % NBUF));
+        if (NBUF == 2 || (tt & 1)) __syncthreads();
     }
     if (MODE == 1) {
 #pragma unroll
