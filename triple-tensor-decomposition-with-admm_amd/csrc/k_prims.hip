@@ -51,26 +51,23 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 // (the driver's RRE, traffic_triple_comparison.m:62-63,194-199).
 //
 // K5's L half on its own: a wave owns one ij-tile (16 rows i of one fibre j,
-// its Khatri-Rao row in registers) and walks the t-tiles; the workgroup's 4
+// its Khatri-Rao row in registers) and walks the t-tiles; the workgroup's 8
 // waves share the C^T slice of each t-tile, staged in LDS double-buffered
 // (the slice of t-tile tt+1 is loaded into registers before tile tt's MFMAs
 // and written after them: one barrier per t-tile).  Per t-tile a wave runs
 // RP/4 f64 MFMAs and stores 4 x 128 B pieces of L (16 consecutive i at 4
-// t-values per store).  Bound: f64 MFMA (2*N*R flops); ~70 VGPRs and 17 KB
-// of LDS per workgroup leave several waves per SIMD to cover the stores and
-// the staging.  (Round 3's form staged 32 t-values per step without double
-// buffering, two barriers each: 0.464 ms at 512^3 r = 8, 0.47 of the MFMA peak.)
+// t-values per store).  Bound: f64 MFMA (2*N*R flops).
+// Measured at 512^3 r = 8 (rocprofv3, tools/round4_tpab.sh, round 4; box to
+// box spread ~10 us): 8 waves 336.5-347.7 us, 4 waves 339-344; four slice
+// buffers with a barrier every second t-tile 353.6; two MFMA accumulation
+// chains 357.0 (the extra LDS and registers cost more occupancy than the
+// barriers save); the factors read in their reference layouts (no pack
+// kernel) 358.5; no LDS at all — one wave per workgroup loading its operands
+// from L2 by buffer loads — 371.7, or 385.9 with the next t-tile's operands
+// prefetched (122 VGPRs).  (Round 3's form staged 32 t-values per step
+// without double buffering, two barriers each: 0.464 ms.)
 // ---------------------------------------------------------------------------
-#ifndef TP_WV
-#define TP_WV 4
-#endif
-constexpr int TP_WAVES = TP_WV;
-#ifndef TP_NBUF
-#define TP_NBUF 2
-#endif
-#ifndef TP_CHAINS
-#define TP_CHAINS 1
-#endif
+constexpr int TP_WAVES = 8;
 
 template <int RP, int MODE>
 __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__ Ah,
@@ -85,10 +82,7 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
     constexpr int NT = 64 * TP_WAVES;
     constexpr int SP = RP * 8;  // d2v pairs per slice (RP rows of 16 t)
     constexpr int NS = (SP + NT - 1) / NT;
-    // four slice buffers staged two t-tiles ahead: a barrier after every
-    // second t-tile only (K5's scheme, k_admm.hip)
-    constexpr int NBUF = TP_NBUF, SD = NBUF / 2;  // slices staged SD t-tiles ahead
-    __shared__ double sct[NBUF][RP * SK];
+    __shared__ double sct[2][RP * SK];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int il = lane & 15, tg = lane >> 4;
     const int64_t tile = (int64_t)blockIdx.x * TP_WAVES + wid;
@@ -128,50 +122,35 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
     };
     const int64_t obase = i + ldj * j;
     double sn = 0.0, sd = 0.0;
-    for (int q = 0; q < SD; ++q)
-        if (q < ntt) {
-            stage_load(q);
-            stage_store(q);
-        }
+    stage_load(0);
+    stage_store(0);
     __syncthreads();
     for (int64_t tt = 0; tt < ntt; ++tt) {
-        const int buf = (int)(tt % NBUF);
-        const bool more = tt + SD < ntt;
-        if (more) stage_load(tt + SD);
+        const int buf = (int)(tt & 1);
+        const bool more = tt + 1 < ntt;
+        if (more) stage_load(tt + 1);
         const double* cT = sct[buf];
-        // two accumulation chains (even / odd K-steps), summed once
-        d4 acc = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-        if (TP_CHAINS == 2) {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int s = 0; s < KS; s += 2) {
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + 4 + tg) * SK + il], kr[s + 1], acc1, 0, 0, 0);
-            }
-            acc += acc1;
-        } else {
-#pragma unroll
-            for (int s = 0; s < KS; ++s)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
-        }
+        for (int s = 0; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(cT[(4 * s + tg) * SK + il], kr[s], acc, 0, 0, 0);
         // C/D element r of lane l: L(i, j, t = 16 tt + (l>>4) + 4r)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t t = tt * 16 + tg + 4 * r;
+        for (int rr = 0; rr < 4; ++rr) {
+            const int64_t t = tt * 16 + tg + 4 * rr;
             if (!row_ok || t >= n3) continue;
             const int64_t off = obase + ldt * t;
             if (MODE == 0) {
-                __builtin_nontemporal_store(acc[r], L + off);
+                __builtin_nontemporal_store(acc[rr], L + off);
             } else {
                 const double x = X[off];
-                const double dlt = acc[r] - x;
+                const double dlt = acc[rr] - x;
                 sn = fma(dlt, dlt, sn);
                 sd = fma(x, x, sd);
             }
         }
-        // the slice two t-tiles ahead into the buffer read two t-tiles ago;
-        // one of any two consecutive steps ends at the barrier
-        if (more) stage_store((int)((tt + SD) % NBUF));
-        if (NBUF == 2 || (tt & 1)) __syncthreads();
+        if (more) stage_store(buf ^ 1);  // buf^1 was last read in t-tile tt-1
+        __syncthreads();
     }
     if (MODE == 1) {
 #pragma unroll
@@ -205,14 +184,14 @@ void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* 
     if (bhj < 0) bhj = g.RP;
     if (g.n3p % 16) throw Error(TRITD_ERR_ARG, "triple_product: n3p must be a multiple of 16");
     const dim3 grid(tp_grid(g)), block(64 * TP_WAVES);
-#define TP_CASE(RPV)                                                                            \
-    case RPV:                                                                                   \
-        if (mode == 0)                                                                          \
-            hipLaunchKernelGGL((k_tp<RPV, 0>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
-                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt, ahj, bhj);                  \
-        else                                                                                    \
-            hipLaunchKernelGGL((k_tp<RPV, 1>), grid, block, 0, st, Ah, Bh, ChT, Lout, X, partial, \
-                               g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt, ahj, bhj);                  \
+#define TP_CASE(RPV)                                                                                 \
+    case RPV:                                                                                        \
+        if (mode == 0)                                                                               \
+            hipLaunchKernelGGL((k_tp<RPV, 0>), grid, block, 0, st, Ah, Bh, ChT, Lout, X,      \
+                               partial, g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt, ahj, bhj);      \
+        else                                                                                         \
+            hipLaunchKernelGGL((k_tp<RPV, 1>), grid, block, 0, st, Ah, Bh, ChT, Lout, X,      \
+                               partial, g.n1p, g.n1l, g.n3, g.n3p, g.tiles, ldj, ldt, ahj, bhj);      \
         break;
     switch (g.RP) {
         TP_CASE(16)
