@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4 close-out: the full GPU suite, smoke() and the default bench line.
+set -uo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/round4_final; mkdir -p $O
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests_full.log 2>&1 || { tail -30 $O/gpu_tests_full.log; exit 1; }
+tail -1 $O/gpu_tests_full.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python -u bench.py > $O/bench_line.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cut -c1-400 $O/bench_line.json

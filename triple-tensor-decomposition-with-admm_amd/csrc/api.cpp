@@ -38,6 +38,10 @@ tritd_status fail(tritd_status s, const std::string& m) {
 template <class F>
 tritd_status guarded(F&& f) {
     try {
+        // hipGetLastError (TRITD_CHECK_LAUNCH) reports the thread's last error
+        // from any caller: one left by an earlier, unrelated call (the host
+        // program's, or an ignored failure in a destructor) is not this call's
+        (void)hipGetLastError();
         f();
         g_last_error.clear();
         return TRITD_OK;

@@ -67,7 +67,10 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 // prefetched (122 VGPRs).  (Round 3's form staged 32 t-values per step
 // without double buffering, two barriers each: 0.464 ms.)
 // ---------------------------------------------------------------------------
-constexpr int TP_WAVES = 8;
+#ifndef TP_WV
+#define TP_WV 8
+#endif
+constexpr int TP_WAVES = TP_WV;
 
 template <int RP, int MODE>
 __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__ Ah,
