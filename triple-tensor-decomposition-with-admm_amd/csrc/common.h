@@ -27,7 +27,17 @@ struct Error : std::runtime_error {
                                  std::string(#expr) + ": " + hipGetErrorString(e_));        \
     } while (0)
 
-#define TRITD_CHECK_LAUNCH() TRITD_HIP(hipGetLastError())
+// a launch's error, named by the launching site
+#define TRITD_STR2_(x) #x
+#define TRITD_STR_(x) TRITD_STR2_(x)
+#define TRITD_CHECK_LAUNCH()                                                                 \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess)                                                                \
+            throw ::tritd::Error(TRITD_ERR_HIP, std::string("kernel launch at " __FILE__ ":" \
+                                                            TRITD_STR_(__LINE__) ": ") +     \
+                                                    hipGetErrorString(e_));                  \
+    } while (0)
 
 __host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 __host__ __device__ inline int64_t cdiv(int64_t x, int64_t m) { return (x + m - 1) / m; }

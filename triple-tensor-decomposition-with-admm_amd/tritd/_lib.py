@@ -8,6 +8,7 @@ raise `TritdError`.
 from __future__ import annotations
 
 import ctypes as C
+import importlib.util
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -123,7 +124,29 @@ SIGNATURES = {
 }
 
 
+def _preload_hip_runtime():
+    """One HIP runtime per process.  torch ships its own libamdhip64 (soname
+    libamdhip64.so.7, loaded from torch/lib as libamdhip64.so).  Were
+    libtritd.so loaded first, its libamdhip64.so.7 would bind the system copy
+    and a later `import torch` would load torch's beside it: two runtimes,
+    whose streams are not interchangeable (a torch stream handed to a
+    tritd_dev_* entry point fails to launch with 'invalid argument') and
+    whose device initialisation can collide (torch: 'No HIP GPUs are
+    available') — seen in the GPU suite, round 4 (tools/dbg_bisect.sh).  So
+    load torch's copy first when torch is installed (without importing
+    torch): libtritd and a later torch both bind that one file."""
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+            return
+
+
 def _load():
+    _preload_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libtritd.so not found at {LIB_PATH}: run __graft_entry__.build() "
                           "(or `make` in triple-tensor-decomposition-with-admm_amd/csrc)")
