@@ -189,3 +189,17 @@ def test_product_reads_few_environment_knobs():
             knobs |= set(re.findall(r'getenv\("(TRITD_\w+)"\)', open(os.path.join(csrc, f)).read()))
     assert knobs <= {"TRITD_DENSE_E", "TRITD_PROBE", "TRITD_K5_TSPLIT", "TRITD_FUSED", "TRITD_SHOV"}, knobs
     assert len(knobs) <= 8
+
+
+def test_one_hip_runtime_with_torch():
+    """tritd/_lib.py loads torch's libamdhip64 before libtritd.so, so a later
+    `import torch` binds the same HIP runtime: a process holding two copies
+    gives torch streams that are invalid handles in tritd_dev_* calls."""
+    code = ("import re, sys; sys.path.insert(0, %r); import tritd._lib; import torch; "
+            "print(sorted(set(re.findall(r'/\\S*libamdhip64\\S*', open('/proc/self/maps').read()))))"
+            % os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd"))
+    out = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True,
+                         check=True, timeout=300).stdout.strip().splitlines()[-1]
+    import ast
+    maps = ast.literal_eval(out)  # a list literal printed by the child
+    assert len(maps) == 1, maps
