@@ -75,3 +75,22 @@ def test_dev_product_recreated_stream(env):
     torch.cuda.synchronize(dev)
     for X, s, R, _ in outs:
         assert rel(X.cpu().numpy().reshape(s[:3], order="F"), R) <= 1e-13
+
+
+def test_dev_product_after_shutdown(env):
+    """tritd_shutdown frees the per-stream scratch (after the last product on
+    it finishes); the next device-form call recreates it."""
+    torch, tritd, check, lib = env
+    dev = torch.device("cuda", 0)
+    s = (64, 40, 50, 8)
+    h, t = _case(torch, *s, seed=77)
+    torch.cuda.synchronize(dev)
+    X1 = torch.empty(s[0] * s[1] * s[2], dtype=torch.float64, device=dev)
+    X2 = torch.empty_like(X1)
+    _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X1, 0)
+    lib.tritd_shutdown()  # no synchronisation before it
+    _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X2, 0)
+    torch.cuda.synchronize(dev)
+    R = tritd.triple_product(*h)
+    for X in (X1, X2):
+        assert rel(X.cpu().numpy().reshape(s[:3], order="F"), R) <= 1e-13

@@ -165,7 +165,10 @@ double* scratch(ScratchSet& s, int slot, size_t count) {
 
 void drop_scratch() {
     std::lock_guard<std::mutex> lk(g_scratch_mutex);
-    if (g_scratch) g_scratch->clear();
+    if (!g_scratch) return;
+    for (auto& kv : *g_scratch)  // the last product on each stream may still read its buffers
+        if (kv.second.done) (void)hipEventSynchronize(kv.second.done);
+    g_scratch->clear();
 }
 
 void drop_comms() {
