@@ -165,30 +165,28 @@ def primitives(device, n=512, r=8, reps=10):
     (unfold.m:6-10, modes 2 and 3), soft_threshold (soft_threshold.m:2) at
     >= 80 % of HBM, and triple_product (triple_product.m:6, called by both
     drivers after the solve) on f64 MFMA — on device-resident n^3 fp64 arrays,
-    timed with HIP events on the stream they are launched on."""
+    timed with HIP events on the stream they are launched on (the null
+    stream), through the HIP runtime libtritd is bound to (tritd.hip)."""
     import ctypes as C
-    import torch
+    from tritd import hip
     from tritd._lib import check, lib
-    dev = torch.device("cuda", device)
-    st = torch.cuda.current_stream(dev)
-    sp = C.c_void_p(st.cuda_stream)
+    hip.set_device(device)
+    sp = C.c_void_p(0)
     N = n ** 3
-    g = torch.Generator(device=dev).manual_seed(0)
-    X = torch.randn(N, dtype=torch.float64, device=dev, generator=g)
-    Y = torch.empty_like(X)
-    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    rng = np.random.default_rng(0)
+    X = hip.DeviceArray.from_host(rng.standard_normal(N))
+    Y = hip.DeviceArray(N * 8)
+    p = lambda t: C.c_void_p(t.ptr)  # noqa: E731
+    ev = hip.EventTimer(None)
 
     def timed(fn, warm=3):
         for _ in range(warm):
             fn()
-        torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
+        hip.synchronize()
+        ev.start()
         for _ in range(reps):
             fn()
-        e1.record(st)
-        torch.cuda.synchronize(dev)
-        return e0.elapsed_time(e1) / reps
+        return ev.stop() / reps
 
     out = {"shape": [n, n, n], "r": r, "reps": reps}
 
@@ -209,14 +207,14 @@ def primitives(device, n=512, r=8, reps=10):
     ms = timed(lambda: check(lib.tritd_dev_soft_threshold_f64(p(X), N, C.c_double(0.5), p(Y), sp)))
     rec("soft_threshold", ms, 2 * N * 8)
     R = r * r
-    A = torch.randn(n * R, dtype=torch.float64, device=dev, generator=g)
-    B = torch.randn(R * n, dtype=torch.float64, device=dev, generator=g)
-    Cc = torch.randn(R * n, dtype=torch.float64, device=dev, generator=g)
+    A = hip.DeviceArray.from_host(rng.standard_normal(n * R))
+    B = hip.DeviceArray.from_host(rng.standard_normal(R * n))
+    Cc = hip.DeviceArray.from_host(rng.standard_normal(R * n))
     ms = timed(lambda: check(lib.tritd_dev_triple_product_f64(p(A), p(B), p(Cc), n, n, n, r, p(Y),
                                                              sp)))
     rec("triple_product", ms, N * 8, 2.0 * N * R)
-    del X, Y, A, B, Cc
-    torch.cuda.empty_cache()
+    for t in (X, Y, A, B, Cc):
+        t.free()
     return out
 
 
@@ -317,9 +315,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     host_comm = args.comm == "host"
 
-    import torch
     dist = None
     if world > 1:
+        # torch only where ranks need torch.distributed (imported before
+        # tritd, so libtritd binds torch's HIP runtime: one per process); one
+        # GPU runs without torch, on /opt/rocm's runtime (tritd._lib)
+        import torch
         import torch.distributed as dist
         if host_comm:
             # rehearsal of the N > 1 path on fewer GPUs than ranks: gloo for
@@ -342,7 +343,8 @@ def main():
         ensure_built()
     barrier()
     import tritd
-    from tritd import synth
+    from tritd import hip, synth
+    from tritd._lib import HIP_RUNTIME
 
     n1, n2, n3, r, dts = CONFIGS[args.config]
     if args.n is not None:
@@ -380,26 +382,26 @@ def main():
         raise SystemExit("communicator reports %d ranks, WORLD_SIZE is %d" % (comm_info[0], world))
 
     # inputs resident in HBM before the timed region
-    dev = torch.device("cuda", local_rank)
-    D_shard = torch.from_numpy(np.ascontiguousarray(D[i0:i1].transpose(2, 1, 0))).to(dev)
+    hip.set_device(local_rank)
+    D_shard = hip.DeviceArray.from_host(np.asfortranarray(D[i0:i1]))
     sess = tritd.Session(r, opts, data["A0"], data["B0"], data["C0"], n1=n1, n2=n2, n3=n3, i0=i0,
-                         i1=i1, d_device_ptr=D_shard.data_ptr(), ldD=i1 - i0, device=local_rank,
+                         i1=i1, d_device_ptr=D_shard.ptr, ldD=i1 - i0, device=local_rank,
                          comm=comm, dtype=npdt)
-    del D_shard
+    D_shard.free()
 
     sess.run(W)
     sess.sync()
     dense0, tiles_per_launch = sess.counters()
     # host-side collectives of the bench itself (gloo wants CPU tensors)
-    cdev = torch.device("cpu") if host_comm else dev
+    cdev = (torch.device("cpu") if host_comm else torch.device("cuda", local_rank)) if dist else None
 
     def timed(k):
         barrier()
-        torch.cuda.synchronize()
+        hip.synchronize()
         t0 = time.perf_counter()
         sess.run(k)
         done, stopped = sess.sync()
-        torch.cuda.synchronize()
+        hip.synchronize()
         barrier()
         dt = time.perf_counter() - t0
         if dist is not None:
@@ -441,8 +443,9 @@ def main():
     # finish the solve (untimed) and report the driver RRE at the final k
     sess.run(maxIter - done)
     k_final, _ = sess.sync()
-    L_shard = torch.from_numpy(np.ascontiguousarray(Lstar[i0:i1].transpose(2, 1, 0))).to(dev)
-    num, den = sess.rre_parts(L_shard.data_ptr(), i1 - i0)
+    L_shard = hip.DeviceArray.from_host(np.asfortranarray(Lstar[i0:i1]))
+    num, den = sess.rre_parts(L_shard.ptr, i1 - i0)
+    L_shard.free()
     if dist is not None:
         t = torch.tensor([num, den], device=cdev, dtype=torch.float64)
         dist.all_reduce(t)
@@ -539,6 +542,8 @@ def main():
                                       + (" (host all-reduce rehearsal: not a scaling number)"
                                          if host_comm and world > 1 else "")},
             "comm": {"transport": comm_info[2], "nranks": comm_info[0]},
+            # the libamdhip64 libtritd ran on (/opt/rocm's without torch)
+            "hip_runtime": HIP_RUNTIME,
             "rccl_nranks": comm_info[0] if comm_info[2] == "rccl" else None,
             "rre_final": rre,
             "k_final": k_final,
@@ -596,10 +601,9 @@ def bench_als(args):
     W = X x3 C^; 4 N R flops on f64 MFMA, N*8 B read)."""
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--algo als runs on one GPU")
-    import torch
     ensure_built()
     import tritd
-    from tritd import synth
+    from tritd import hip, synth
     n1, n2, n3, r, _ = CONFIGS[4]
     if args.n is not None:
         n1 = n2 = n3 = args.n
@@ -607,20 +611,19 @@ def bench_als(args):
     K, W = args.steps, args.warmup
     data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
     X = data["D"]
-    dev = torch.device("cuda", 0)
-    Xd = torch.from_numpy(np.ascontiguousarray(X.transpose(2, 1, 0))).to(dev)
+    Xd = hip.DeviceArray.from_host(np.asfortranarray(X))
     opts = dict(maxIter=K + W, tol=0.0)  # tol 0: the stop test never fires in the timed region
     s = tritd.AlsSession(r, opts, data["A0"], data["B0"], data["C0"], n1=n1, n2=n2, n3=n3,
-                         x_device_ptr=Xd.data_ptr(), ldX=n1, quiet=True)
-    del Xd
+                         x_device_ptr=Xd.ptr, ldX=n1, quiet=True)
+    Xd.free()
     s.run(W)
     s.sync()
     s.set_timing(True)
-    torch.cuda.synchronize()
+    hip.synchronize()
     t0 = time.perf_counter()
     s.run(K)
     done, stopped = s.sync()
-    torch.cuda.synchronize()
+    hip.synchronize()
     dt = time.perf_counter() - t0
     km = s.kernel_ms()
     res = s.get()

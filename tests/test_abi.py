@@ -191,15 +191,59 @@ def test_product_reads_few_environment_knobs():
     assert len(knobs) <= 8
 
 
-def test_one_hip_runtime_with_torch():
-    """tritd/_lib.py loads torch's libamdhip64 before libtritd.so, so a later
-    `import torch` binds the same HIP runtime: a process holding two copies
-    gives torch streams that are invalid handles in tritd_dev_* calls."""
-    code = ("import re, sys; sys.path.insert(0, %r); import tritd._lib; import torch; "
-            "print(sorted(set(re.findall(r'/\\S*libamdhip64\\S*', open('/proc/self/maps').read()))))"
-            % os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd"))
+_MAPS_CHILD = """
+import re, sys, json
+sys.path.insert(0, %(pkg)r)
+order = %(order)r
+if order == "torch_first":
+    import torch
+import tritd._lib as L
+err = None
+if order == "torch_after":
+    import torch
+    try:
+        L.check_one_runtime("probe")
+    except L.TritdError as e:
+        err = str(e)
+maps = open("/proc/self/maps").read()
+libs = lambda name: sorted(set(re.findall(r"(/\\S*%%s\\S*)" %% name, maps)))
+print(json.dumps({"hip": libs("libamdhip64"), "hsa": libs("libhsa-runtime64"),
+                  "rccl": libs("librccl"), "bound": L.HIP_RUNTIME, "err": err}))
+"""
+
+
+def _maps(order):
+    import json
+    code = _MAPS_CHILD % {"pkg": os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd"),
+                          "order": order}
+    env = {k: v for k, v in os.environ.items() if k != "TRITD_HIP_RUNTIME"}
     out = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True,
-                         check=True, timeout=300).stdout.strip().splitlines()[-1]
-    import ast
-    maps = ast.literal_eval(out)  # a list literal printed by the child
-    assert len(maps) == 1, maps
+                         check=True, timeout=300, env=env).stdout.strip().splitlines()[-1]
+    return json.loads(out)
+
+
+def test_hip_runtime_without_torch_is_the_system_one():
+    """No torch in the process: libtritd binds /opt/rocm's HIP runtime (the one
+    it is built against, and the MEX drop-in's), one copy each of the HIP, HSA
+    and RCCL libraries."""
+    m = _maps("no_torch")
+    assert len(m["hip"]) == 1 and m["hip"][0].startswith("/opt/rocm"), m
+    assert m["bound"] == m["hip"][0]
+    assert len(m["hsa"]) == 1 and m["hsa"][0].startswith("/opt/rocm"), m
+    assert len(m["rccl"]) == 1, m
+
+
+def test_hip_runtime_with_torch_imported_first_is_torch_s():
+    """torch imported first: libtritd binds torch's copy — still one runtime,
+    so torch streams and memory are valid in tritd_dev_* calls."""
+    m = _maps("torch_first")
+    assert len(m["hip"]) == 1 and "torch" in m["hip"][0], m
+    assert m["bound"] == m["hip"][0]
+
+
+def test_torch_imported_after_tritd_fails_loudly():
+    """torch imported after tritd (system runtime): two runtimes are mapped,
+    and the device-pointer entry points refuse to run (check_one_runtime)."""
+    m = _maps("torch_after")
+    assert len(m["hip"]) == 2, m
+    assert m["err"] and "two HIP runtimes" in m["err"], m

@@ -207,16 +207,16 @@ def test_config4_determinism_and_stepping(tritd, big):
 
 def test_config4_recovers_low_rank(tritd, big):
     """Driver RRE (traffic_triple_comparison.m:62-63) on the device."""
-    import torch
-    from tritd import synth
+    from tritd import hip, synth
     opts = dict(synth.TRAFFIC_OPTS, maxIter=60)
     n = 512
     s = tritd.Session(8, opts, big["A0"], big["B0"], big["C0"], n1=n, n2=n, n3=n, D=big["D"],
                       device=0)
     s.run(60)
     k, stopped = s.sync()
-    L = torch.from_numpy(np.ascontiguousarray(big["Lstar"].transpose(2, 1, 0))).cuda()
-    num, den = s.rre_parts(L.data_ptr(), n)
+    L = hip.DeviceArray.from_host(np.asfortranarray(big["Lstar"]))
+    num, den = s.rre_parts(L.ptr, n)
+    L.free()
     res = s.get()
     s.close()
     assert k == 60 and not stopped

@@ -17,80 +17,122 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def env():
-    import torch
     import tritd
+    from tritd import hip
     from tritd._lib import check, lib
     assert tritd.device_count() > 0, "no GPU visible: the HIP path must run"
-    return torch, tritd, check, lib
+    return hip, tritd, check, lib
 
 
-def _case(torch, n1, n2, n3, r, seed):
+def _case(hip, n1, n2, n3, r, seed):
     from tritd import synth
     A, B, Cc = synth.random_factors(n1, n2, n3, r, seed=seed)
-    dev = torch.device("cuda", 0)
-    t = [torch.from_numpy(np.asarray(x).ravel(order="F").copy()).to(dev) for x in (A, B, Cc)]
+    t = [hip.DeviceArray.from_host(np.asarray(x).ravel(order="F").copy()) for x in (A, B, Cc)]
     return (A, B, Cc), t
 
 
 def _launch(lib, check, fn, t, dims, X, stream):
-    p = lambda x: C.c_void_p(x.data_ptr())  # noqa: E731
+    p = lambda x: C.c_void_p(x.ptr)  # noqa: E731
     check(fn(p(t[0]), p(t[1]), p(t[2]), *dims, p(X), C.c_void_p(stream)))
+
+
+def _host(X, s):
+    out = np.empty(s[0] * s[1] * s[2])
+    return X.to_host(out).reshape(s[:3], order="F")
 
 
 @pytest.mark.parametrize("model", ["cp", "qi"])
 def test_dev_products_unsynchronised(env, model):
-    torch, tritd, check, lib = env
+    hip, tritd, check, lib = env
     fn = lib.tritd_dev_triple_product_qi_f64 if model == "qi" else lib.tritd_dev_triple_product_f64
-    dev = torch.device("cuda", 0)
     # small then larger shapes (the second grows every scratch buffer), 8 cases
     shapes = [(30, 31, 29, 3), (64, 40, 50, 8), (17, 16, 20, 8), (96, 80, 70, 16)] * 2
-    cases = [_case(torch, *s, seed=11 + q) for q, s in enumerate(shapes)]
+    cases = [_case(hip, *s, seed=11 + q) for q, s in enumerate(shapes)]
     ref = [tritd.triple_product(*h, model=model) for h, _ in cases]
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s1, s2 = hip.Stream(), hip.Stream()
     outs = []
+    hip.synchronize()  # the operands' uploads
     for q, ((h, t), s) in enumerate(zip(cases, shapes)):
-        X = torch.empty(s[0] * s[1] * s[2], dtype=torch.float64, device=dev)
-        st = (0, s1.cuda_stream, s2.cuda_stream)[q % 3]
-        torch.cuda.synchronize(dev)  # the operands were made on the current stream
+        X = hip.DeviceArray(s[0] * s[1] * s[2] * 8)
+        st = (0, s1.handle, s2.handle)[q % 3]
         _launch(lib, check, fn, t, s[:4], X, st)  # no synchronisation between calls
         outs.append(X)
-    torch.cuda.synchronize(dev)
+    hip.synchronize()
     for X, s, R in zip(outs, shapes, ref):
-        got = X.cpu().numpy().reshape(s[:3], order="F")
-        assert rel(got, R) <= 1e-13
+        assert rel(_host(X, s), R) <= 1e-13
 
 
 def test_dev_product_recreated_stream(env):
-    torch, tritd, check, lib = env
-    dev = torch.device("cuda", 0)
+    hip, tritd, check, lib = env
     shapes = [(128, 96, 200, 8), (40, 30, 20, 4), (128, 96, 200, 8)]
     outs = []
     for q, s in enumerate(shapes):
-        h, t = _case(torch, *s, seed=40 + q)
-        torch.cuda.synchronize(dev)
-        st = torch.cuda.Stream(dev)  # a stream per call (torch's pool repeats handles)
-        X = torch.empty(s[0] * s[1] * s[2], dtype=torch.float64, device=dev)
-        _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X, st.cuda_stream)
+        h, t = _case(hip, *s, seed=40 + q)
+        hip.synchronize()
+        st = hip.Stream()  # a stream per call, destroyed after it (handles get reused)
+        X = hip.DeviceArray(s[0] * s[1] * s[2] * 8)
+        _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X, st.handle)
+        st.close()
         outs.append((X, s, tritd.triple_product(*h), t))
-    torch.cuda.synchronize(dev)
+    hip.synchronize()
     for X, s, R, _ in outs:
-        assert rel(X.cpu().numpy().reshape(s[:3], order="F"), R) <= 1e-13
+        assert rel(_host(X, s), R) <= 1e-13
 
 
 def test_dev_product_after_shutdown(env):
     """tritd_shutdown frees the per-stream scratch (after the last product on
     it finishes); the next device-form call recreates it."""
-    torch, tritd, check, lib = env
-    dev = torch.device("cuda", 0)
+    hip, tritd, check, lib = env
     s = (64, 40, 50, 8)
-    h, t = _case(torch, *s, seed=77)
-    torch.cuda.synchronize(dev)
-    X1 = torch.empty(s[0] * s[1] * s[2], dtype=torch.float64, device=dev)
-    X2 = torch.empty_like(X1)
+    h, t = _case(hip, *s, seed=77)
+    hip.synchronize()
+    X1 = hip.DeviceArray(s[0] * s[1] * s[2] * 8)
+    X2 = hip.DeviceArray(X1.nbytes)
     _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X1, 0)
     lib.tritd_shutdown()  # no synchronisation before it
     _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X2, 0)
-    torch.cuda.synchronize(dev)
+    hip.synchronize()
     R = tritd.triple_product(*h)
     for X in (X1, X2):
-        assert rel(X.cpu().numpy().reshape(s[:3], order="F"), R) <= 1e-13
+        assert rel(_host(X, s), R) <= 1e-13
+
+
+_TORCH_CHILD = """
+import sys, ctypes as C
+sys.path.insert(0, %(pkg)r)
+import numpy as np
+import torch                      # first: tritd then binds torch's HIP runtime
+import tritd
+from tritd import synth
+from tritd._lib import check, lib, hip_runtimes
+assert len(hip_runtimes()) == 1, hip_runtimes()
+dev = torch.device("cuda", 0)
+A, B, Cc = synth.random_factors(64, 40, 50, 8, seed=5)
+t = [torch.from_numpy(np.asarray(x).ravel(order="F").copy()).to(dev) for x in (A, B, Cc)]
+X = torch.empty(64 * 40 * 50, dtype=torch.float64, device=dev)
+st = torch.cuda.Stream(dev)
+torch.cuda.synchronize(dev)
+p = lambda x: C.c_void_p(x.data_ptr())
+check(lib.tritd_dev_triple_product_f64(p(t[0]), p(t[1]), p(t[2]), 64, 40, 50, 8, p(X),
+                                       C.c_void_p(st.cuda_stream)))
+torch.cuda.synchronize(dev)
+R = tritd.triple_product(A, B, Cc)
+got = X.cpu().numpy().reshape(64, 40, 50, order="F")
+err = np.linalg.norm(got - R) / np.linalg.norm(R)
+assert err <= 1e-13, err
+print("torch interop ok", hip_runtimes()[0])
+"""
+
+
+def test_dev_product_on_torch_memory_and_stream():
+    """A torch host (torch imported first): tritd binds torch's HIP runtime,
+    and a device-form product on torch tensors and a torch stream gives the
+    host form's result.  In a child process: this suite's own process stays
+    on /opt/rocm's runtime (tests/test_zz_runtime.py)."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    r = subprocess.run([sys.executable, "-c", _TORCH_CHILD % {"pkg": PKG}], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "torch interop ok" in r.stdout and "torch" in r.stdout

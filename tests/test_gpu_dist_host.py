@@ -79,9 +79,21 @@ def _worker(rank, world, port, spec, outdir):
 
 
 def _run(tmp_path, world, spec):
-    import torch.multiprocessing as mp
-    mp.start_processes(_worker, args=(world, _free_port(), spec, str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    # stdlib spawn (not torch.multiprocessing): the ranks import torch for
+    # gloo, this test process does not (it stays on /opt/rocm's HIP runtime)
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(q, world, port, spec, str(tmp_path))) for q in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(200)
+    for p in ps:
+        if p.is_alive():
+            p.terminate()
+            p.join()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
     return [np.load(tmp_path / f"rank{q}.npz") for q in range(world)]
 
 

@@ -1,7 +1,7 @@
 """Dense-E K5 form (TRITD_DENSE_E=1) against the C restatement over a sweep of
 shapes, 3 iterations each: which dimension breaks it.  Diagnostic.
 
-    python tools/diag_de.py
+    python tools/rounds/r4/diag_de.py
 """
 import os
 import subprocess

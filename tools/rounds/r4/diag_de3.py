@@ -2,7 +2,7 @@
 few iterations on the same input, located by (i, j, t) and tile coordinates.
 Diagnostic.
 
-    python tools/diag_de3.py [n1 n2 n3 iters]
+    python tools/rounds/r4/diag_de3.py [n1 n2 n3 iters]
 """
 import os
 import sys

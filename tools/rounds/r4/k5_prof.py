@@ -1,6 +1,6 @@
 """Timing experiment: K5's t-walk phase clocks (s_memtime) from a K5_PROF=1
 build, on the bench workload.
-usage: TRITD_LIB=ab/prof.so python tools/k5_prof.py"""
+usage: TRITD_LIB=ab/prof.so python tools/rounds/r4/k5_prof.py"""
 import ctypes as C
 import os
 import sys

@@ -1,6 +1,6 @@
 """Dev helper: K5 time and placement-probe results vs the shard's row count
 (config-4 problem, session over rows [0, rows)).
-usage: python tools/k5_rows.py rows[@i0][:ENV=V,ENV=V] ...  (env knobs set for that session only)"""
+usage: python tools/rounds/r4/k5_rows.py rows[@i0][:ENV=V,ENV=V] ...  (env knobs set for that session only)"""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -59,13 +59,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(void* p, int bytes) {
                "buffer_load_dwordx4 v[60:63], %[vo], %[rl], %[so] offen offset:3072 nt\n" \
                "v_fma_f64 v[20:21], %[a], 1.0, 0\nv_fma_f64 v[22:23], %[b], 1.0, 0\n"
 #define FILL FILL_NOP
-#define PROBE_ASM(NT, OVER)                                                                  \
+#define PROBE_ASM(NT, OVER) PROBE_ASM_ST("buffer_store_dwordx4 v[20:23], %[vo], %[rs], %[so] offen" NT "\n", OVER)
+// ST: the store itself (SGPR soffset as K5's streams, a constant soffset —
+// the case LLVM pads — or a global store)
+#define ST_SGPR "buffer_store_dwordx4 v[20:23], %[vo], %[rs], %[so] offen nt\n"
+#define ST_CONST "buffer_store_dwordx4 v[20:23], %[vt], %[rs], 0 offen nt\n"
+#define ST_GLOBAL "global_store_dwordx4 %[ga], v[20:23], off nt\n"
+#define PROBE_ASM_ST(STORE, OVER)                                                            \
     asm volatile("" PRE                                                                      \
-                 "buffer_store_dwordx4 v[20:23], %[vo], %[rs], %[so] offen" NT "\n"         \
+                 STORE                                                                      \
                  FILL OVER                                                                  \
                  :                                                                          \
                  : [a] "v"(a), [b] "v"(b), [j] "v"(junk), [vo] "v"(voff), [rs] "s"(r),     \
-                   [so] "s"(soff), [k] "i"(K), [la] "v"(laddr), [ro] "s"(rj), [rl] "s"(rld)  \
+                   [so] "s"(soff), [k] "i"(K), [la] "v"(laddr), [ro] "s"(rj), [rl] "s"(rld),  \
+                   [ga] "v"(gaddr + it * 128), [vt] "v"(voff + it * 1024)                                                     \
                  : "v20", "v21", "v22", "v23", "v30", "v31", "v32", "v33", "v40", "v41", "v42", "v43", \
                    "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", \
                    "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "memory")
@@ -77,6 +84,8 @@ __global__ __launch_bounds__(256) void probe(double* out) {
     double* base = out + (size_t)wave * ITERS * 128;
     const __amdgpu_buffer_rsrc_t r = rsrc_of(base, ITERS * 1024);
     const int voff = lane * 16;
+    // ST_CONST / ST_GLOBAL: the tile offset goes into the address instead
+    double* gaddr = base + 2 * lane;
     // an LDS word and a global word holding junk, read back into the data
     // registers of the in-flight store (OP 4 / OP 5)
     __shared__ double lj[64];
@@ -135,6 +144,14 @@ __global__ __launch_bounds__(256) void probe(double* out) {
             if constexpr (OP == 3) PROBE_ASM(" nt", "");
             if constexpr (OP == 4) PROBE_ASM(" nt", "ds_read_b64 v[20:21], %[la]\ns_waitcnt lgkmcnt(0)\n");
             if constexpr (OP == 5) PROBE_ASM(" nt", "buffer_load_dwordx2 v[20:21], %[vo], %[ro], 0 offen\ns_waitcnt vmcnt(0)\n");
+            // round 5: the compiler's own K5 sequences (k_admm.hip built with
+            // TRITD_STORE_KEEP=0: a 64-bit VALU write of the first data pair
+            // right behind a buffer_store_dwordx4 with an SGPR soffset)
+            if constexpr (OP == 6) PROBE_ASM(" nt", "v_lshl_add_u64 v[20:21], %[j], 0, %[j]\n");
+            if constexpr (OP == 7) PROBE_ASM(" nt", "v_add_f64 v[22:23], %[j], %[j]\n");  // the second pair
+            if constexpr (OP == 8) PROBE_ASM_ST(ST_CONST, "v_add_f64 v[20:21], %[j], %[j]\n");
+            if constexpr (OP == 9) PROBE_ASM_ST(ST_GLOBAL, "v_add_f64 v[20:21], %[j], %[j]\n");
+            if constexpr (OP == 10) PROBE_ASM_ST(ST_SGPR, "v_fma_f64 v[20:21], %[j], %[j], %[j]\n");
 #undef PRE
 #define PRE PRE_NOP
         } else if constexpr (AUX == 2) {
@@ -159,7 +176,7 @@ void run(double* d, std::vector<double>& h, int blocks, const char* name) {
     CHECK(hipGetLastError());
     CHECK(hipDeviceSynchronize());
     CHECK(hipMemcpy(h.data(), d, n * sizeof(double), hipMemcpyDeviceToHost));
-    long bad = 0, bad_lane[16] = {0};
+    long bad = 0, bad_lane[16] = {0}, bad_w[2] = {0, 0};
     for (int wave = 0; wave < blocks * 4; ++wave)
         for (int it = 0; it < ITERS; ++it)
             for (int lane = 0; lane < 64; ++lane) {
@@ -168,12 +185,14 @@ void run(double* d, std::vector<double>& h, int blocks, const char* name) {
                 const double* p = &h[((size_t)wave * ITERS + it) * 128 + 2 * lane];
                 if (p[0] != a || p[1] != -a) {
                     ++bad;
+                    bad_w[0] += p[0] != a;
+                    bad_w[1] += p[1] != -a;
                     ++bad_lane[lane & 15];
                 }
             }
     std::printf("%-28s K=%2d aux=%d dp=%d fl=%d  wrong %ld of %zu", name, K, AUX, DP, FL, bad, n / 2);
     if (bad) {
-        std::printf("  by lane%%16:");
+        std::printf("  words %ld/%ld  by lane%%16:", bad_w[0], bad_w[1]);
         for (int l = 0; l < 16; ++l) std::printf(" %ld", bad_lane[l]);
     }
     std::printf("\n");
@@ -190,20 +209,20 @@ int main() {
     }
     std::vector<double> h(n);
     run<0, 3, 0>(d, h, blocks, "control");
-    run<1, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<2, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<3, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<4, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<6, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<8, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<12, 2, 2, 1, 6>(d, h, blocks, "loads in flight, v_nop");
-    run<1, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
-    run<2, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
-    run<3, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
-    run<4, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
-    run<6, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
-    run<8, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
-    run<12, 2, 2, 1, 7>(d, h, blocks, "loads in flight, DP adds x2");
+    // round 5: the writers the compiler placed behind K5's stores
+    run<0, 2, 2, 1>(d, h, blocks, "sgpr soff, v_add_f64");
+    run<1, 2, 2, 1>(d, h, blocks, "sgpr soff, v_add_f64");
+    run<0, 6, 2, 1>(d, h, blocks, "sgpr soff, v_lshl_add_u64");
+    run<1, 6, 2, 1>(d, h, blocks, "sgpr soff, v_lshl_add_u64");
+    run<0, 10, 2, 1>(d, h, blocks, "sgpr soff, v_fma_f64");
+    run<1, 10, 2, 1>(d, h, blocks, "sgpr soff, v_fma_f64");
+    run<0, 7, 2, 1>(d, h, blocks, "sgpr soff, 2nd pair add");
+    run<1, 7, 2, 1>(d, h, blocks, "sgpr soff, 2nd pair add");
+    // the store forms the compiler pads (one wait state)
+    run<0, 8, 2, 1>(d, h, blocks, "const soff, v_add_f64");
+    run<1, 8, 2, 1>(d, h, blocks, "const soff, v_add_f64");
+    run<0, 9, 2, 1>(d, h, blocks, "global, v_add_f64");
+    run<1, 9, 2, 1>(d, h, blocks, "global, v_add_f64");
     CHECK(hipFree(d));
     return 0;
 }

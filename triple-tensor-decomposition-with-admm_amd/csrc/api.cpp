@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "als.h"
+#include "group.h"
 #include "solver.h"
 
 using namespace tritd;
@@ -113,7 +114,7 @@ int pick_device(int32_t device) {
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Device set of the one-shot entry points (tritd_set_devices), and the RCCL
-// communicators of a set of distinct devices (ncclCommInitAll): created on
+// communicators of a set of distinct devices (group_comms): created on
 // first use, kept in this process-global context until the set changes or
 // tritd_shutdown (SURVEY.md §8b Ownership).
 std::vector<int> g_devices;
@@ -126,7 +127,7 @@ std::vector<ncclComm_t> g_comms;
 // one stream are ordered by it and reuse its buffers.  Heap-held and never
 // destroyed at exit (the HIP runtime may be gone by then); tritd_shutdown
 // frees it.  (Stream-ordered hipMallocAsync scratch on the null stream read
-// back as zeros on a repeated call on ROCm 7.2: tools/iso_tp.sh, round 4.)
+// back as zeros on a repeated call on ROCm 7.2: tools/rounds/r4/iso_tp.sh, round 4.)
 // The entry's `done` event marks the end of the last call's kernels: a call
 // waits on it (device side) before overwriting the buffers, which orders it
 // after that call even when a destroyed stream's handle is reused.
@@ -171,22 +172,59 @@ void drop_scratch() {
     g_scratch->clear();
 }
 
+// Wait out a non-blocking communicator's "in progress" state (its
+// initialisation, an enqueue, a finalize); any other state is returned.
+ncclResult_t nccl_settle(ncclComm_t c) {
+    ncclResult_t a = ncclInProgress;
+    while (a == ncclInProgress) {
+        const ncclResult_t q = ncclCommGetAsyncError(c, &a);
+        if (q != ncclSuccess) return q;
+        if (a == ncclInProgress) std::this_thread::yield();
+    }
+    return a;
+}
+
 void drop_comms() {
     for (ncclComm_t c : g_comms)
-        if (c) (void)ncclCommDestroy(c);
+        if (c) {
+            const ncclResult_t f = ncclCommFinalize(c);
+            if (f == ncclSuccess || f == ncclInProgress) (void)nccl_settle(c);
+            (void)ncclCommDestroy(c);
+        }
     g_comms.clear();
     g_comm_devs.clear();
 }
 
+// The communicators of a set of distinct devices: what ncclCommInitAll
+// builds, but NON-BLOCKING (config.blocking = 0), so that no call of a shard
+// thread waits inside RCCL for a peer — the device group's abort protocol
+// (group.h: GroupAbort) relies on it.  Created from this thread in one group.
 void group_comms(const std::vector<int>& devs) {
     if (g_comm_devs == devs && !g_comms.empty()) return;
     drop_comms();
-    g_comms.assign(devs.size(), nullptr);
-    const ncclResult_t r = ncclCommInitAll(g_comms.data(), (int)devs.size(), devs.data());
-    if (r != ncclSuccess) {
-        g_comms.clear();
-        throw Error(TRITD_ERR_RCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    const int P = (int)devs.size();
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) throw Error(TRITD_ERR_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::vector<ncclComm_t> cs((size_t)P, nullptr);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    r = ncclGroupStart();
+    for (int p = 0; p < P && (r == ncclSuccess || r == ncclInProgress); ++p) {
+        TRITD_HIP(hipSetDevice(devs[p]));
+        r = ncclCommInitRankConfig(&cs[p], P, id, p, &cfg);
     }
+    const ncclResult_t re = ncclGroupEnd();
+    if (r == ncclInProgress) r = ncclSuccess;
+    if (r == ncclSuccess && re != ncclInProgress) r = re;
+    for (int p = 0; p < P && r == ncclSuccess; ++p)
+        if (cs[p]) r = nccl_settle(cs[p]);
+    if (r != ncclSuccess) {
+        for (ncclComm_t c : cs)
+            if (c) (void)ncclCommAbort(c);
+        throw Error(TRITD_ERR_RCCL, std::string("ncclCommInitRankConfig (device group): ") + ncclGetErrorString(r));
+    }
+    g_comms = cs;
     g_comm_devs = devs;
 }
 
@@ -239,7 +277,10 @@ struct DeviceGroup {
             TRITD_HIP(hipSetDevice(devs[p]));
             rr = ncclAllReduce(buf[p], buf[p], (size_t)count, ncclFloat64, ncclSum, g_comms[p], st[p]);
         }
-        const ncclResult_t re = ncclGroupEnd();
+        ncclResult_t re = ncclGroupEnd();
+        if (rr == ncclInProgress) rr = ncclSuccess;  // non-blocking communicators (group_comms)
+        if (re == ncclInProgress) re = ncclSuccess;
+        for (int p = 0; p < P && rr == ncclSuccess && re == ncclSuccess; ++p) re = nccl_settle(g_comms[p]);
         if (rr != ncclSuccess || re != ncclSuccess)
             throw Error(TRITD_ERR_RCCL, std::string("grouped ncclAllReduce: ") +
                                             ncclGetErrorString(rr != ncclSuccess ? rr : re));
@@ -264,76 +305,24 @@ struct DeviceGroup {
     }
 };
 
-// In-process all-reduce of a device group whose shards share a GPU (one
-// device repeated: RCCL refuses a GPU twice in one communicator): the host
-// transport of each shard's session lands here, on that shard's host thread.
-// Sums run in shard order (s = b0; s += b1; ...), like the device-side
-// virtual-shard sum.  abort() wakes every waiter with a failure, so a shard
-// that throws never leaves the others blocked in a collective.
-struct ThreadReducer {
-    struct Rank {
-        ThreadReducer* r;
-        int rank;
-    };
-    int P;
-    std::vector<Rank> ranks;
-    std::vector<double*> bufs;
-    std::mutex m;
-    std::condition_variable cv;
-    int arrived = 0;
-    uint64_t gen = 0;
-    bool aborted = false;
-    explicit ThreadReducer(int p) : P(p), bufs(p, nullptr) {
-        for (int q = 0; q < p; ++q) ranks.push_back({this, q});
-    }
-    bool barrier() {
-        std::unique_lock<std::mutex> lk(m);
-        if (aborted) return false;
-        const uint64_t g = gen;
-        if (++arrived == P) {
-            arrived = 0;
-            ++gen;
-            cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return gen != g || aborted; });
-        }
-        return !aborted;
-    }
-    void abort() {
-        std::lock_guard<std::mutex> lk(m);
-        aborted = true;
-        cv.notify_all();
-    }
-    // tritd_allreduce_fn
-    static int32_t allreduce(double* buf, int64_t count, int32_t op, void* user) {
-        Rank* rk = static_cast<Rank*>(user);
-        ThreadReducer* r = rk->r;
-        r->bufs[rk->rank] = buf;
-        if (!r->barrier()) return 1;
-        if (rk->rank == 0) {  // the others wait at the next barrier
-            for (int64_t e = 0; e < count; ++e) {
-                double v = r->bufs[0][e];
-                for (int q = 1; q < r->P; ++q) v = op ? std::fmax(v, r->bufs[q][e]) : v + r->bufs[q][e];
-                for (int q = 0; q < r->P; ++q) r->bufs[q][e] = v;
-            }
-        }
-        return r->barrier() ? 0 : 1;
-    }
-};
-
 // Drive one session per shard of a device group, each on its own host thread
-// (shard 0 on the calling thread: a host print callback such as mexPrintf
-// stays on the host's thread), all through a communicator: RCCL
-// communicators from ncclCommInitAll for distinct devices, the in-process
-// ThreadReducer for one device repeated.  shard(p, comm) builds, runs and
-// reads back shard p and returns its TRITD_FLAG_* bits.  A shard that throws
-// aborts the others' collectives (ncclCommAbort / ThreadReducer::abort), so
-// no thread stays blocked; the first error is rethrown here.
+// (group.h: run_shard_threads; shard 0 on the calling thread), all through a
+// communicator: the group's non-blocking RCCL communicators (group_comms) for
+// distinct devices, the in-process ThreadReducer for one device repeated.
+// shard(p, comm) builds, runs and reads back shard p and returns its
+// TRITD_FLAG_* bits.  A shard that throws aborts the group: the ThreadReducer
+// wakes its waiters; the RCCL communicators are aborted under the group's
+// abort protocol (GroupAbort), after which no shard touches them again — a
+// shard blocked on its stream is released by the abort and fails at its next
+// all-reduce.  The aborted communicators leave the cache once every thread
+// has joined.  The first error is rethrown.
 template <class F>
 void run_threaded(DeviceGroup& grp, F&& shard) {
     const int P = grp.size();
     std::unique_ptr<ThreadReducer> red;
+    std::unique_ptr<GroupAbort> ga;
     if (grp.same) red.reset(new ThreadReducer(P));
+    else ga.reset(new GroupAbort(P));
     std::vector<tritd_comm> comms((size_t)P);
     for (int p = 0; p < P; ++p) {
         comms[p].nranks = P;
@@ -344,41 +333,35 @@ void run_threaded(DeviceGroup& grp, F&& shard) {
             comms[p].host_user = &red->ranks[p];
         } else {
             comms[p].comm = g_comms[p];  // owned by the cache (group_comms)
+            comms[p].group = ga.get();
         }
     }
-    std::vector<std::exception_ptr> err((size_t)P);
     std::vector<uint32_t> fl((size_t)P, 0);
-    bool aborted_rccl = false;
-    std::mutex abort_m;
     auto abort_all = [&] {
         if (red) {
             red->abort();
             return;
         }
-        std::lock_guard<std::mutex> lk(abort_m);
-        if (aborted_rccl) return;
-        aborted_rccl = true;
-        // unblocks the other shards' collectives; the communicators are gone
-        for (ncclComm_t c : g_comms)
-            if (c) (void)ncclCommAbort(c);
-        g_comms.clear();
-        g_comm_devs.clear();
+        ga->abort([&](int p) {
+            if (comms[p].comm) (void)ncclCommAbort(comms[p].comm);  // frees it
+            comms[p].comm = nullptr;
+        });
     };
-    auto body = [&](int p) {
-        try {
-            TRITD_HIP(hipSetDevice(grp.devs[p]));
-            fl[p] = shard(p, &comms[p]);
-        } catch (...) {
-            err[p] = std::current_exception();
-            abort_all();
+    try {
+        run_shard_threads(
+            P,
+            [&](int p) {
+                TRITD_HIP(hipSetDevice(grp.devs[p]));
+                fl[p] = shard(p, &comms[p]);
+            },
+            abort_all);
+    } catch (...) {
+        if (ga && ga->aborted()) {  // every thread has joined: forget the freed communicators
+            g_comms.clear();
+            g_comm_devs.clear();
         }
-    };
-    std::vector<std::thread> th;
-    for (int p = 1; p < P; ++p) th.emplace_back(body, p);
-    body(0);
-    for (auto& t : th) t.join();
-    for (int p = 0; p < P; ++p)
-        if (err[p]) std::rethrow_exception(err[p]);
+        throw;
+    }
     for (int p = 0; p < P; ++p) g_last_flags |= fl[p];
 }
 
@@ -388,7 +371,7 @@ void run_threaded(DeviceGroup& grp, F&& shard) {
 // bench.py and the multi-rank tests run (the fused single-stream iteration
 // with two all-reduces per iteration, or its side-stream form for fp32 / Qi /
 // r > 8).  Distinct devices all-reduce over RCCL (communicators from
-// ncclCommInitAll, cached); one device repeated uses the in-process
+// group_comms, cached); one device repeated uses the in-process
 // ThreadReducer.  Shard 0 runs on the calling thread, so `disp` prints (the
 // MEX's mexPrintf) stay on the host's own thread.  D, O, E are column-major
 // n1 x n2 x n3 host arrays of es-byte elements.

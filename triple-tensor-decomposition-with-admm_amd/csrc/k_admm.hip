@@ -72,8 +72,11 @@ static constexpr int K5_WPE = 2;
 // stores: round 2 interleaved A/B, nt stores -1.5 % iteration, nt loads a
 // further -0.9 % (M1 then finds W still in the Infinity Cache).
 static constexpr int K5_NT_AUX = 2;
-#ifndef K5_ORD
-#define K5_ORD 0  // experiment: dense-E branch after the L MFMAs, E encode after the W MFMAs
+// 1: the data of every wide store is held live past a later point (below,
+// DESIGN.md §4.2).  0 exists only so that tests/test_isa_store_war.py can
+// build the kernel without the keeps and check that its scan catches them.
+#ifndef TRITD_STORE_KEEP
+#define TRITD_STORE_KEEP 1
 #endif
 
 #if TRITD_WTRACE
@@ -444,7 +447,7 @@ void k5_fused(K5Args a) {
             // with the L MFMAs)
             dn = ce_decode(cx.ce, lane, img, ev);
             dp = ce_decode(cx.cep, lane, imgp, evp);
-            if (!K5_ORD) dense_fix(tt, dn, dp, ev, evp);
+            dense_fix(tt, dn, dp, ev, evp);
             if (pf) load_slot(tt + 2, cx);  // cx.ce and cx.cep were consumed above
         }
         double tr[4], En[4];
@@ -475,9 +478,6 @@ void k5_fused(K5Args a) {
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int s = 0; s < KS; ++s) lacc = mfma4(opL(buf, s), kr[s], lacc);
-            // (K5_ORD: the decode's LDS round trips share a basic block with
-            // the L MFMAs; the rare dense branch follows them)
-            if (K5_ORD && !DE) dense_fix(tt, dn, dp, ev, evp);
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 d2v YLn2;
@@ -525,7 +525,7 @@ void k5_fused(K5Args a) {
                 __builtin_nontemporal_store(d2v{En[0], En[1]}, Ep2 + o);
                 __builtin_nontemporal_store(d2v{En[2], En[3]}, Ep2 + o + 64);
                 ++ndense;
-            } else if (!K5_ORD) {
+            } else {
                 ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
             }
             keep[2] = d2v{En[0], En[1]};
@@ -545,7 +545,7 @@ void k5_fused(K5Args a) {
             keep[4 + p] = tv;
         }
         // Y_L and E data live until here (past the T transpose and stores)
-        asm volatile("" ::"v"(keep[0]), "v"(keep[1]), "v"(keep[2]), "v"(keep[3]));
+        if (TRITD_STORE_KEEP) asm volatile("" ::"v"(keep[0]), "v"(keep[1]), "v"(keep[2]), "v"(keep[3]));
         // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4);
         // the C/D register of T is directly the B operand
 #pragma unroll
@@ -553,11 +553,8 @@ void k5_fused(K5Args a) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
                 wacc[m] = mfma4(opW(buf, r, m), tr[r], wacc[m]);
-        // (K5_ORD: the encode's LDS round trips after the W MFMAs, its rare
-        // dense-store branch last)
-        if constexpr (K5_ORD && !PRO && !DE) ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
         // T data live until here (past the W MFMAs)
-        asm volatile("" ::"v"(keep[4]), "v"(keep[5]));
+        if (TRITD_STORE_KEEP) asm volatile("" ::"v"(keep[4]), "v"(keep[5]));
         // the slice SD t-tiles ahead into the buffer read SD t-tiles ago
         if (ps) stage_store(slice_buf(tt + SD - t0));
         if (bar) __syncthreads();
@@ -656,7 +653,7 @@ int k5_grid(const Geom& g) { return (int)cdiv(g.tiles, K5_WAVES); }
 // almost idle, so the walk is cut into chunks of >= 4 t-tiles until there are
 // about 256 workgroups; each chunk's W is a partial set that M1 / M2 sum as
 // they read W.  (Config 2, round 4: 18 chunks of 4 against 9 of 8, iteration
-// 0.106 vs 0.114 ms; 36 of 2: 0.113 ms — tools/round4_c2_tsplit.sh.)
+// 0.106 vs 0.114 ms; 36 of 2: 0.113 ms — tools/rounds/r4/round4_c2_tsplit.sh.)
 int k5_tsplit(const Geom& g) {
     if (g.RP > 64) return 1;
     const int64_t wg = cdiv(g.tiles, K5_WAVES);

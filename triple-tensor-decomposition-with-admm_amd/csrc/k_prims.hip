@@ -57,7 +57,7 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 // and written after them: one barrier per t-tile).  Per t-tile a wave runs
 // RP/4 f64 MFMAs and stores 4 x 128 B pieces of L (16 consecutive i at 4
 // t-values per store).  Bound: f64 MFMA (2*N*R flops).
-// Measured at 512^3 r = 8 (rocprofv3, tools/round4_tpab.sh, round 4; box to
+// Measured at 512^3 r = 8 (rocprofv3, tools/rounds/r4/round4_tpab.sh, round 4; box to
 // box spread ~10 us): 8 waves 336.5-347.7 us, 4 waves 339-344; four slice
 // buffers with a barrier every second t-tile 353.6; two MFMA accumulation
 // chains 357.0 (the extra LDS and registers cost more occupancy than the

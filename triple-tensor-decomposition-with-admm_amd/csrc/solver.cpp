@@ -10,6 +10,7 @@
 // the session stream; virtual-shard groups (api.cpp) sum the red buffers of
 // several sessions on one device instead.
 #include "solver.h"
+#include "group.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <sys/mman.h>
@@ -616,7 +617,31 @@ void populate_output(void* p, size_t bytes) {
     for (auto& t : th) t.join();
 }
 
+// ncclResult_t as GroupAbort::enqueue reads it: 0 done, 1 in progress, else
+// 100 + the error
+int nccl_state(ncclResult_t r) {
+    return r == ncclSuccess ? 0 : r == ncclInProgress ? 1 : 100 + (int)r;
+}
+
 void comm_allreduce(tritd_comm* c, double* buf, int64_t count, bool max, hipStream_t st) {
+    if (c->group) {  // a device-group shard: the communicator only under the abort protocol
+        const int s = c->group->enqueue(
+            c->rank,
+            [&] {
+                return nccl_state(ncclAllReduce(buf, buf, (size_t)count, ncclFloat64,
+                                                max ? ncclMax : ncclSum, c->comm, st));
+            },
+            [&] {
+                ncclResult_t a = ncclSuccess;
+                const ncclResult_t q = ncclCommGetAsyncError(c->comm, &a);
+                return nccl_state(q != ncclSuccess ? q : a);
+            });
+        if (s < 0)
+            throw Error(TRITD_ERR_RCCL, "all-reduce not issued: another shard of the device group failed");
+        if (s != 0)
+            throw Error(TRITD_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString((ncclResult_t)(s - 100)));
+        return;
+    }
     if (c->comm) {
         const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclFloat64,
                                              max ? ncclMax : ncclSum, c->comm, st);

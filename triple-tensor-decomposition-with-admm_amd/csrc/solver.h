@@ -7,12 +7,19 @@
 
 #include "kernels.h"
 
+namespace tritd {
+class GroupAbort;
+}
+
 struct tritd_comm {
-    ncclComm_t comm = nullptr;             // RCCL (tritd_comm_create)
+    ncclComm_t comm = nullptr;             // RCCL (tritd_comm_create; group_comms)
     tritd_allreduce_fn host_fn = nullptr;  // or a host transport (tritd_comm_create_host)
     void* host_user = nullptr;
     int nranks = 1, rank = 0, device = 0;
-    bool active() const { return comm != nullptr || host_fn != nullptr; }
+    // a shard of a device group driven by run_threaded: its non-blocking RCCL
+    // communicator is used only through the group's abort protocol (group.h)
+    tritd::GroupAbort* group = nullptr;
+    bool active() const { return comm != nullptr || host_fn != nullptr || group != nullptr; }
 };
 
 namespace tritd {

@@ -10,11 +10,14 @@ from __future__ import annotations
 import ctypes as C
 import importlib.util
 import os
+import re
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TRITD_LIB", os.path.join(HERE, "libtritd.so"))
 
 OK = 0
+TRITD_ERR_HIP = 3
 STATUS_NAMES = {0: "TRITD_OK", 1: "TRITD_ERR_ARG", 2: "TRITD_ERR_OPTS", 3: "TRITD_ERR_HIP",
                 4: "TRITD_ERR_RCCL", 5: "TRITD_ERR_NOMEM", 6: "TRITD_ERR_NODEV",
                 7: "TRITD_ERR_UNSUPPORTED", 8: "TRITD_ERR_STATE"}
@@ -124,25 +127,64 @@ SIGNATURES = {
 }
 
 
-def _preload_hip_runtime():
-    """One HIP runtime per process.  torch ships its own libamdhip64 (soname
-    libamdhip64.so.7, loaded from torch/lib as libamdhip64.so).  Were
-    libtritd.so loaded first, its libamdhip64.so.7 would bind the system copy
-    and a later `import torch` would load torch's beside it: two runtimes,
-    whose streams are not interchangeable (a torch stream handed to a
-    tritd_dev_* entry point fails to launch with 'invalid argument') and
-    whose device initialisation can collide (torch: 'No HIP GPUs are
-    available') — seen in the GPU suite, round 4 (tools/dbg_bisect.sh).  So
-    load torch's copy first when torch is installed (without importing
-    torch): libtritd and a later torch both bind that one file."""
+def _torch_lib_dir():
+    """torch's bundled lib directory, without importing torch."""
+    t = sys.modules.get("torch")
+    if t is not None and getattr(t, "__file__", None):
+        return os.path.join(os.path.dirname(t.__file__), "lib")
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.submodule_search_locations:
+        return None
+    return os.path.join(list(spec.submodule_search_locations)[0], "lib")
+
+
+def hip_runtimes():
+    """Distinct libamdhip64 files mapped into this process (/proc/self/maps)."""
+    try:
+        maps = open("/proc/self/maps").read()
+    except OSError:
+        return []
+    return sorted(set(re.findall(r"(/\S*libamdhip64\S*)", maps)))
+
+
+def _preload_hip_runtime():
+    """Choose the HIP runtime libtritd binds: ONE per process.
+
+    libtritd.so is built against /opt/rocm's HIP and needs libamdhip64.so.7;
+    by default the loader binds /opt/rocm's copy (RPATH) — the runtime the
+    MATLAB/MEX drop-in uses.  torch ships its own copy (torch/lib, same
+    soname), and a process holding both has two runtimes whose streams are not
+    interchangeable (a torch stream in a tritd_dev_* call fails to launch;
+    torch's device init can fail — round 4, tools/rounds/r4/dbg_bisect.sh).  So:
+      * torch already imported (sys.modules): bind torch's copy, the one
+        mapped already;
+      * TRITD_HIP_RUNTIME=torch: bind torch's copy before torch is imported
+        (a host that will import torch later);
+      * otherwise (TRITD_HIP_RUNTIME unset / "system"): /opt/rocm's.
+    A host that imports torch AFTER tritd on the system runtime gets two
+    runtimes: check_one_runtime() (called by the device-pointer entry points
+    of the Python API) then fails with a message saying so."""
+    mode = os.environ.get("TRITD_HIP_RUNTIME", "auto")
+    if mode not in ("auto", "torch", "system"):
+        raise ImportError(f"TRITD_HIP_RUNTIME={mode!r}: expected 'torch' or 'system'")
+    if mode == "system" or (mode == "auto" and "torch" not in sys.modules):
         return
-    for d in spec.submodule_search_locations:
-        p = os.path.join(d, "lib", "libamdhip64.so")
-        if os.path.exists(p):
-            C.CDLL(p, mode=C.RTLD_GLOBAL)
-            return
+    d = _torch_lib_dir()
+    p = os.path.join(d, "libamdhip64.so") if d else None
+    if p and os.path.exists(p):
+        C.CDLL(p, mode=C.RTLD_GLOBAL)
+    elif mode == "torch":
+        raise ImportError("TRITD_HIP_RUNTIME=torch but torch's libamdhip64 was not found")
+
+
+def check_one_runtime(where):
+    """Fail loudly when the process maps two HIP runtimes (torch imported
+    after tritd on the system runtime): device pointers and streams of one are
+    not valid in the other."""
+    rts = hip_runtimes()
+    if len(rts) > 1:
+        raise TritdError(TRITD_ERR_HIP, f"{where}: two HIP runtimes in this process ({', '.join(rts)}); "
+                         "import torch before tritd, or set TRITD_HIP_RUNTIME=torch")
 
 
 def _load():
@@ -159,6 +201,8 @@ def _load():
 
 
 lib = _load()
+# the libamdhip64 libtritd is bound to (recorded by bench.py's line)
+HIP_RUNTIME = next((p for p in hip_runtimes()), None)
 
 
 def check(status):

@@ -410,6 +410,7 @@ class Session:
         if probe:
             flags |= _lib.SESSION_PROBE
         if d_device_ptr is not None:
+            _lib.check_one_runtime("Session(d_device_ptr=...)")
             dptr = C.c_void_p(int(d_device_ptr))
             flags |= _lib.SESSION_D_ON_DEVICE
             ldD = ldD if ldD is not None else (i1 - i0)
@@ -454,6 +455,7 @@ class Session:
         return dict(A=A, B=B, C=Cf, O=O, E=E, errHist=eh[: k.value].copy(), k=k.value)
 
     def rre_parts(self, dX_ptr, ldX):
+        _lib.check_one_runtime("Session.rre_parts")
         num, den = C.c_double(0), C.c_double(0)
         fn = lib.tritd_session_rre_parts_f32 if self.f32 else lib.tritd_session_rre_parts
         check(fn(self._s, C.c_void_p(int(dX_ptr)), int(ldX), C.byref(num), C.byref(den)))
