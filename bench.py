@@ -218,6 +218,35 @@ def primitives(device, n=512, r=8, reps=10):
     return out
 
 
+def config5_leg(steps, warmup=2):
+    """`bench.py --config 5` for `steps` timed iterations in a child process
+    (its own device memory; host data generated there), reduced to the keys
+    that place it beside the config-4 line: iters/s, ms per iteration, K5
+    against the f32 MFMA peak, K2, final RRE."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", "5", "--steps", str(steps),
+           "--warmup", str(warmup), "--no-cpu", "--no-e2e", "--no-prims", "--no-c5"]
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=480)
+    except subprocess.TimeoutExpired:
+        return {"error": "config-5 leg timed out (480 s)"}
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": "config-5 leg failed (rc %d): %s" % (p.returncode, p.stderr[-500:])}
+    d = json.loads(lines[-1])
+    roof = d["roofline"]
+    return {"workload": d["config"]["workload"], "value": d["value"], "unit": d["unit"],
+            "ms_per_step": d["ms_per_step"], "steps": d["steps"], "warmup": d["warmup"],
+            "dtype": d["dtype"], "rre_final": d["rre_final"], "k_final": d["k_final"],
+            "fused_update_ms": d["kernel_ms"]["fused_update"],
+            "mode3_mttkrp_ms": d["kernel_ms"]["mode3_mttkrp"],
+            "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
+                                                  "kernel", "traffic", "traffic_source",
+                                                  "algorithmic_flops_per_launch")},
+            "mode3_mfma_frac": roof.get("mfma_gemm", {}).get("frac"),
+            "wall_s": round(time.perf_counter() - t0, 1)}
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -288,6 +317,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end one-shot calls")
     ap.add_argument("--no-prims", action="store_true", help="skip the primitive kernels")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the config-5 leg of the default (config 4, N = 1) line")
+    ap.add_argument("--c5-steps", type=int, default=10, help="timed iterations of the config-5 leg")
     ap.add_argument("--comm", default="rccl", choices=("rccl", "host"),
                     help="N > 1: libtritd's RCCL communicator (default), or the host all-reduce "
                          "transport over gloo (correctness rehearsal with ranks sharing a GPU)")
@@ -365,7 +397,9 @@ def main():
     elif args.config == 3:  # RRE of the low-rank part against the frames
         data = synth.video_like(n1, n2, n3, r, seed=0, init_seed=123)
         data["Lstar"] = data.pop("X")
-    else:  # config 5 uses the same recipe, rounded to single
+    elif f32:  # config 5: the same recipe, rounded to single, streamed
+        data = synth.low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    else:
         data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
     D, Lstar = data["D"].astype(npdt, order="F"), data["Lstar"].astype(npdt, order="F")
     del data["D"], data["Lstar"]
@@ -432,13 +466,28 @@ def main():
     # K2 and whole-iteration event timings: an untimed sample right after the
     # timed region (the solve continues; events around every kernel there)
     n_more = min(10, maxIter - done)
+    ar_ms, ar_n = 0.0, 0
     if n_more > 0:
         sess.set_timing(True)
         sess.run(n_more)
         sess.sync()
         km2 = sess.kernel_ms()
         km["mode3"], km["iteration"] = km2["mode3"], km2["iteration"]
+        ar_ms, ar_n = sess.comm_ms()
         sess.set_timing(False)
+    # per-rank breakdown of that sample (N > 1): the all-reduces' ms (issue to
+    # completion on the session stream, waiting for the slowest rank
+    # included) and the rest of the iteration (this rank's compute)
+    per_rank = None
+    if dist is not None:
+        mine = torch.tensor([rank, i1 - i0, km["iteration"], ar_ms, ar_n, km["fused_update"]],
+                            dtype=torch.float64, device=cdev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        per_rank = [{"rank": int(v[0]), "rows": int(v[1]), "iteration_ms": float(v[2]),
+                     "allreduce_ms": float(v[3]), "allreduces_per_iteration": int(v[4]),
+                     "compute_ms": float(v[2] - v[3]), "fused_update_ms": float(v[5])}
+                    for v in (t.cpu() for t in allv)]
 
     # finish the solve (untimed) and report the driver RRE at the final k
     sess.run(maxIter - done)
@@ -520,6 +569,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], cpu_iters)
 
+    # the north_star's second headline configuration in the same line
+    # (VERDICT r4 next 5): a bounded config-5 run in a child process, after
+    # this process has released its device memory
+    c5 = None
+    if (rank == 0 and world == 1 and args.config == 4 and args.n is None and args.r is None
+            and not args.no_c5):
+        c5 = config5_leg(args.c5_steps)
+
     if rank == 0:
         line = {
             "metric": "ADMM iters/sec + final RRE, 512^3 r=8 tensor at 1/2/4/8 MI355X",
@@ -545,6 +602,8 @@ def main():
             # the libamdhip64 libtritd ran on (/opt/rocm's without torch)
             "hip_runtime": HIP_RUNTIME,
             "rccl_nranks": comm_info[0] if comm_info[2] == "rccl" else None,
+            # N > 1: per rank, from an events sample after the timed region
+            "per_rank": per_rank,
             "rre_final": rre,
             "k_final": k_final,
             "errHist_final": errhist_final,
@@ -564,6 +623,8 @@ def main():
             "end_to_end": e2e,
             # unfold / soft_threshold / triple_product on 512^3 fp64, device-resident
             "primitives": prims,
+            # config 5 (2048x2048x256 fp32 r=16), a bounded run of its own
+            "config5": c5,
         }
         print(json.dumps(line), flush=True)
 

@@ -181,6 +181,13 @@ enum { TRITD_TIMING_ALL = 1, TRITD_TIMING_K5 = 2 };
 tritd_status tritd_session_set_timing(tritd_session* s, int32_t enable);
 tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, double* mode3_ms,
                                      double* iteration_ms, int32_t* samples);
+/* All-reduce time of the timed iterations (TRITD_TIMING_ALL, a session with
+ * a communicator): the mean ms per iteration spent between
+ * issuing the iteration's all-reduces and their completion on the session
+ * stream (waiting for the slowest rank included), and how many all-reduces
+ * an iteration issued (0 without a communicator).  Per-rank breakdown of
+ * bench.py's N > 1 line: iteration ms - all-reduce ms = compute. */
+tritd_status tritd_session_comm_ms(tritd_session* s, double* allreduce_ms, int32_t* per_iteration);
 /* Placement probe of the session's tensor pool: the probe
  * time (ms) of each candidate pool that was tried (up to cap entries) and
  * the index kept.  *n = 1 when probing was skipped. */

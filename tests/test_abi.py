@@ -247,3 +247,34 @@ def test_torch_imported_after_tritd_fails_loudly():
     m = _maps("torch_after")
     assert len(m["hip"]) == 2, m
     assert m["err"] and "two HIP runtimes" in m["err"], m
+
+
+_KFD_CHILD = """
+import os, sys
+sys.path.insert(0, %(pkg)r)
+from tritd import _lib
+def kfd():
+    for f in os.listdir('/proc/self/fd'):
+        try:
+            if os.readlink('/proc/self/fd/' + f) == '/dev/kfd':
+                return True
+        except OSError:
+            pass
+    return False
+_lib.lib.tritd_version(); _lib.lib.tritd_last_error()
+before = kfd()
+n = _lib.device_count()
+print(before, kfd(), n)
+"""
+
+
+@pytest.mark.gpu
+def test_host_only_entry_points_do_not_initialise_hip():
+    """an entry point that needs no GPU (tritd_version,
+    tritd_last_error) leaves the HIP runtime uninitialised (no /dev/kfd
+    open), so a host may query the library before it launches workers; the
+    first device call initialises it."""
+    code = _KFD_CHILD % {"pkg": os.path.join(ROOT, "triple-tensor-decomposition-with-admm_amd")}
+    out = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True,
+                         check=True, timeout=300).stdout.split()
+    assert out[0] == "False" and out[1] == "True" and int(out[2]) >= 1, out

@@ -63,3 +63,11 @@ def test_bench_two_ranks_from_plain_shell():
     assert line["n_gpus"] == 2
     assert line["comm"] == {"transport": "host", "nranks": 2}
     assert line["value"] > 0 and line["rre_final"] < 1e-3
+    # the per-rank breakdown: each rank's rows, iteration,
+    # all-reduce and compute ms, two all-reduces per iteration
+    pr = line["per_rank"]
+    assert [p["rank"] for p in pr] == [0, 1] and sum(p["rows"] for p in pr) == 64
+    for p in pr:
+        assert p["allreduces_per_iteration"] == 2
+        assert 0 < p["allreduce_ms"] < p["iteration_ms"]
+        assert abs(p["compute_ms"] + p["allreduce_ms"] - p["iteration_ms"]) < 1e-9

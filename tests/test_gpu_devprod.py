@@ -136,3 +136,28 @@ def test_dev_product_on_torch_memory_and_stream():
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "torch interop ok" in r.stdout and "torch" in r.stdout
+
+
+def test_dev_products_on_more_streams_than_the_scratch_cap(env):
+    """The per-(device, stream) scratch cache is bounded (api.cpp SCRATCH_CAP
+    = 16): products on 24 streams, round-robin twice, evict and
+    recreate entries while earlier products may still run, and each result is
+    still the host form's."""
+    hip, tritd, check, lib = env
+    s = (48, 40, 36, 8)
+    cases = [_case(hip, *s, seed=200 + q) for q in range(4)]
+    refs = [tritd.triple_product(*h) for h, _ in cases]
+    streams = [hip.Stream() for _ in range(24)]
+    hip.synchronize()
+    outs = []
+    for rep in range(2):
+        for q, st in enumerate(streams):
+            h, t = cases[q % 4]
+            X = hip.DeviceArray(s[0] * s[1] * s[2] * 8)
+            _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X, st.handle)
+            outs.append((X, q % 4))
+    hip.synchronize()
+    for X, c in outs:
+        assert rel(_host(X, s), refs[c]) <= 1e-13
+    for st in streams:
+        st.close()

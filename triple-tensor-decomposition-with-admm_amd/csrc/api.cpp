@@ -4,6 +4,7 @@
 // message, and never writes its inputs.
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <condition_variable>
 #include <cstdlib>
@@ -36,13 +37,19 @@ tritd_status fail(tritd_status s, const std::string& m) {
     return s;
 }
 
+// set once this library has touched the HIP runtime (pick_device): before
+// that, an entry point does not call into HIP at all, so a host-only call
+// (tritd_version, a host-transport tritd_comm_info, ...) leaves the process
+// without a HIP runtime initialised
+std::atomic<bool> g_hip_used{false};
+
 template <class F>
 tritd_status guarded(F&& f) {
     try {
         // hipGetLastError (TRITD_CHECK_LAUNCH) reports the thread's last error
         // from any caller: one left by an earlier, unrelated call (the host
         // program's, or an ignored failure in a destructor) is not this call's
-        (void)hipGetLastError();
+        if (g_hip_used.load(std::memory_order_relaxed)) (void)hipGetLastError();
         f();
         g_last_error.clear();
         return TRITD_OK;
@@ -96,7 +103,14 @@ void need(const void* p, const char* what) {
     if (!p) throw Error(TRITD_ERR_ARG, std::string(what) + " is NULL");
 }
 
+// first HIP use of an entry point: from here on guarded() clears the
+// thread's stale HIP error before each call; this call's is cleared now
+void hip_entry() {
+    if (!g_hip_used.exchange(true, std::memory_order_relaxed)) (void)hipGetLastError();
+}
+
 int pick_device(int32_t device) {
+    hip_entry();
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
         throw Error(TRITD_ERR_NODEV, "no HIP device visible (libtritd has no CPU fallback)");
@@ -131,27 +145,72 @@ std::vector<ncclComm_t> g_comms;
 // The entry's `done` event marks the end of the last call's kernels: a call
 // waits on it (device side) before overwriting the buffers, which orders it
 // after that call even when a destroyed stream's handle is reused.
+// Bounded: at most SCRATCH_CAP entries; a new (device, stream)
+// beyond that evicts the least recently used entry after its last product
+// has finished (its event).  Each entry has its own lock, held over one
+// call's enqueue (two host threads on one stream would otherwise interleave
+// their packs and products); the map's lock is held only to find, insert or
+// evict an entry, so calls on different streams do not serialise.
 struct ScratchSet {
     std::array<DBuf, 5> buf;
     hipEvent_t done = nullptr;
+    std::mutex m;
+    uint64_t used = 0;  // LRU stamp (under g_scratch_mutex)
+    int busy = 0;       // calls holding or waiting for m (under g_scratch_mutex)
     ~ScratchSet() {
         if (done) (void)hipEventDestroy(done);
     }
 };
+constexpr size_t SCRATCH_CAP = 16;
 std::mutex g_scratch_mutex;
-std::map<std::pair<int, hipStream_t>, ScratchSet>* g_scratch = nullptr;
+std::map<std::pair<int, hipStream_t>, std::unique_ptr<ScratchSet>>* g_scratch = nullptr;
+uint64_t g_scratch_clock = 0;
 
-// the caller holds g_scratch_mutex over the whole enqueue (two host threads
-// on one stream would otherwise interleave their packs and products)
-ScratchSet& scratch_set(hipStream_t st) {
-    if (!g_scratch) g_scratch = new std::map<std::pair<int, hipStream_t>, ScratchSet>();
-    int dev = 0;
-    TRITD_HIP(hipGetDevice(&dev));
-    ScratchSet& s = (*g_scratch)[{dev, st}];
-    if (!s.done) TRITD_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-    else TRITD_HIP(hipStreamWaitEvent(st, s.done, 0));
-    return s;
-}
+// One call's hold on the (device, stream) entry: its lock for the enqueue.
+class ScratchLease {
+public:
+    explicit ScratchLease(hipStream_t st) {
+        int dev = 0;
+        TRITD_HIP(hipGetDevice(&dev));
+        {
+            std::lock_guard<std::mutex> lk(g_scratch_mutex);
+            if (!g_scratch) g_scratch = new std::map<std::pair<int, hipStream_t>, std::unique_ptr<ScratchSet>>();
+            auto& slot = (*g_scratch)[{dev, st}];
+            if (!slot) {
+                evict_locked();
+                slot.reset(new ScratchSet());
+            }
+            s_ = slot.get();
+            s_->used = ++g_scratch_clock;
+            ++s_->busy;
+        }
+        lk_ = std::unique_lock<std::mutex>(s_->m);
+        if (!s_->done) TRITD_HIP(hipEventCreateWithFlags(&s_->done, hipEventDisableTiming));
+        else TRITD_HIP(hipStreamWaitEvent(st, s_->done, 0));
+    }
+    ~ScratchLease() {
+        lk_.unlock();
+        std::lock_guard<std::mutex> lk(g_scratch_mutex);
+        --s_->busy;
+    }
+    ScratchSet& set() { return *s_; }
+
+private:
+    // the least recently used idle entry leaves once the map is full
+    static void evict_locked() {
+        if (g_scratch->size() < SCRATCH_CAP) return;
+        auto victim = g_scratch->end();
+        for (auto it = g_scratch->begin(); it != g_scratch->end(); ++it)
+            if (it->second && it->second->busy == 0 &&
+                (victim == g_scratch->end() || it->second->used < victim->second->used))
+                victim = it;
+        if (victim == g_scratch->end()) return;  // all in use: grow past the cap
+        if (victim->second->done) (void)hipEventSynchronize(victim->second->done);
+        g_scratch->erase(victim);
+    }
+    ScratchSet* s_ = nullptr;
+    std::unique_lock<std::mutex> lk_;
+};
 
 double* scratch(ScratchSet& s, int slot, size_t count) {
     DBuf& b = s.buf[slot];
@@ -167,9 +226,15 @@ double* scratch(ScratchSet& s, int slot, size_t count) {
 void drop_scratch() {
     std::lock_guard<std::mutex> lk(g_scratch_mutex);
     if (!g_scratch) return;
-    for (auto& kv : *g_scratch)  // the last product on each stream may still read its buffers
-        if (kv.second.done) (void)hipEventSynchronize(kv.second.done);
-    g_scratch->clear();
+    for (auto it = g_scratch->begin(); it != g_scratch->end();) {
+        if (it->second && it->second->busy) {  // a call on another thread holds it
+            ++it;
+            continue;
+        }
+        // the last product on the stream may still read the buffers
+        if (it->second && it->second->done) (void)hipEventSynchronize(it->second->done);
+        it = g_scratch->erase(it);
+    }
 }
 
 // Wait out a non-blocking communicator's "in progress" state (its
@@ -768,6 +833,15 @@ tritd_status tritd_session_kernel_ms(tritd_session* s, double* fused_update_ms, 
     });
 }
 
+tritd_status tritd_session_comm_ms(tritd_session* s, double* allreduce_ms, int32_t* per_iteration) {
+    return guarded([&] {
+        need(s, "session");
+        int n = 0;
+        reinterpret_cast<Session*>(s)->comm_ms(allreduce_ms, &n);
+        if (per_iteration) *per_iteration = n;
+    });
+}
+
 tritd_status tritd_session_probe(tritd_session* s, double* ms, int32_t cap, int32_t* n,
                                  int32_t* picked) {
     return guarded([&] {
@@ -1081,13 +1155,14 @@ tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, cons
                                           int64_t n1, int64_t n2, int64_t n3, int32_t r, double* X,
                                           void* stream) {
     return guarded([&] {
+        hip_entry();  // device pointers from the caller: HIP is in use
         check_dims(n1, n2, n3, r, true);
         need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
         hipStream_t st = as_stream(stream);
         Geom g = make_geom(n1, n2, n3, 0, n1, r);
         g.RP = padded_rank32(g.R);  // 16..256: the kernel is instantiated for every padded rank
-        std::lock_guard<std::mutex> lk(g_scratch_mutex);
-        ScratchSet& ss = scratch_set(st);
+        ScratchLease lease(st);
+        ScratchSet& ss = lease.set();
         double* Ah = scratch(ss, 0, (size_t)(g.n1p * g.RP));
         double* Bh = scratch(ss, 1, (size_t)(n2 * g.RP));
         double* ChT = scratch(ss, 2, (size_t)g.RP * g.n3p);
@@ -1102,13 +1177,14 @@ tritd_status tritd_dev_triple_product_qi_f64(const double* A, const double* B, c
                                              int64_t n1, int64_t n2, int64_t n3, int32_t r,
                                              double* X, void* stream) {
     return guarded([&] {
+        hip_entry();  // device pointers from the caller: HIP is in use
         check_dims(n1, n2, n3, r, true);
         need(A, "A"); need(B, "B"); need(C, "C"); need(X, "X");
         hipStream_t st = as_stream(stream);
         Geom g = make_geom(n1, n2, n3, 0, n1, r);
         g.RP = padded_rank32(g.R);
-        std::lock_guard<std::mutex> lk(g_scratch_mutex);
-        ScratchSet& ss = scratch_set(st);
+        ScratchLease lease(st);
+        ScratchSet& ss = lease.set();
         double* Ah = scratch(ss, 0, (size_t)(g.n1p * g.RP));
         double* Bh = scratch(ss, 1, (size_t)(n2 * g.RP));
         double* ChT = scratch(ss, 2, (size_t)g.RP * g.n3p);
@@ -1164,6 +1240,7 @@ tritd_status tritd_triple_product_f64(const double* A, const double* B, const do
 tritd_status tritd_dev_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n3, int32_t mode,
                                   double* Xn, void* stream) {
     return guarded([&] {
+        hip_entry();  // device pointers from the caller: HIP is in use
         if (mode < 1 || mode > 3) throw Error(TRITD_ERR_ARG, "Mode must be 1, 2, or 3.");  // unfold.m:12
         if (n1 <= 0 || n2 <= 0 || n3 <= 0) throw Error(TRITD_ERR_ARG, "tensor dimensions must be positive");
         need(X, "X"); need(Xn, "Xn");
@@ -1198,6 +1275,7 @@ tritd_status tritd_unfold_f64(const double* X, int64_t n1, int64_t n2, int64_t n
 tritd_status tritd_dev_soft_threshold_f64(const double* X, int64_t n, double lam, double* Y,
                                           void* stream) {
     return guarded([&] {
+        hip_entry();  // device pointers from the caller: HIP is in use
         if (n < 0) throw Error(TRITD_ERR_ARG, "n must be >= 0");
         if (n == 0) return;
         need(X, "X"); need(Y, "Y");
@@ -1246,6 +1324,7 @@ tritd_status tritd_dev_evaluate_f64(const double* X, int64_t n, const double* gt
                                     const uint8_t* mask, double* rmse, double* nrmse,
                                     void* stream) {
     return guarded([&] {
+        hip_entry();  // device pointers from the caller: HIP is in use
         if (n < 0 || m < 0) throw Error(TRITD_ERR_ARG, "sizes must be >= 0");
         need(rmse, "rmse"); need(nrmse, "nrmse");
         if (!mask && m != n) throw Error(TRITD_ERR_ARG, "Arrays have incompatible sizes for this operation.");
@@ -1307,6 +1386,7 @@ tritd_status tritd_dev_quality_f64(const double* X1, const double* X2, int64_t n
                                    int64_t nf, double* psnr, double* ssim, double* psnr_frames,
                                    double* ssim_frames, void* stream) {
     return guarded([&] {
+        hip_entry();  // device pointers from the caller: HIP is in use
         if (n1 <= 0 || n2 <= 0 || nf <= 0) throw Error(TRITD_ERR_ARG, "sizes must be positive");
         need(X1, "X1"); need(X2, "X2"); need(psnr, "psnr"); need(ssim, "ssim");
         hipStream_t st = as_stream(stream);

@@ -659,7 +659,10 @@ void comm_allreduce(tritd_comm* c, double* buf, int64_t count, bool max, hipStre
 
 void Session::allreduce(double* buf, int64_t count) {
     if (!comm_ || !comm_->active()) return;
+    const int a = ar_in_iter_++;
+    if (a < EV_AR) mark(6 + 2 * a);
     comm_allreduce(comm_, buf, count, false, st_);
+    if (a < EV_AR) mark(7 + 2 * a);
 }
 
 // Every rank must issue each all-reduce with the same count.  red1 and red2
@@ -1065,14 +1068,17 @@ void Session::run(int iters) {
             // slots: 0 iteration start, 1/2 K2, 3/4 K5, 5 iteration end; at
             // TRITD_TIMING_K5 only 3/4 exist (each record is a stream marker
             // that widens the gap to the next kernel by several us)
-            for (int e = 0; e < 6; ++e) {
+            const bool ar = comm_ && comm_->active();
+            for (int e = 0; e < EV_SLOTS; ++e) {
                 hipEvent_t ev = nullptr;
-                if (timing_ == TRITD_TIMING_ALL || e == 3 || e == 4) TRITD_HIP(hipEventCreate(&ev));
+                if ((timing_ == TRITD_TIMING_ALL && (e < 6 || ar)) || e == 3 || e == 4)
+                    TRITD_HIP(hipEventCreate(&ev));
                 ev_.push_back(ev);
             }
             ev_iter_.push_back(k);
             mark(0);
         }
+        ar_in_iter_ = 0;
         Range it_range("tritd:iteration");
         if (fused_) {
             iterate_fused(k);
@@ -1090,6 +1096,7 @@ void Session::run(int iters) {
             phaseD(k);
         }
         mark(5);
+        ar_in_iter_ = EV_AR;  // all-reduces outside the iteration (a flush) are not timed
         maybe_print(k);
         maybe_dense_e(k);
     }
@@ -1097,11 +1104,23 @@ void Session::run(int iters) {
 }
 
 void Session::harvest_timing() {
-    for (size_t b = 0; b + 6 <= ev_.size(); b += 6) {
+    for (size_t b = 0; b + EV_SLOTS <= ev_.size(); b += EV_SLOTS) {
         float it = 0, m3 = 0, k5 = 0;
         if (ev_[b]) TRITD_HIP(hipEventElapsedTime(&it, ev_[b], ev_[b + 5]));
         if (ev_[b + 1]) TRITD_HIP(hipEventElapsedTime(&m3, ev_[b + 1], ev_[b + 2]));
         TRITD_HIP(hipEventElapsedTime(&k5, ev_[b + 3], ev_[b + 4]));
+        int nar = 0;
+        for (int a = 0; a < EV_AR; ++a) {
+            hipEvent_t e0 = ev_[b + 6 + 2 * a], e1 = ev_[b + 7 + 2 * a];
+            if (!e0 || !e1 || hipEventQuery(e1) != hipSuccess) continue;  // not recorded this iteration
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) {
+                acc_ar_ += ms;
+                ++nar;
+            }
+        }
+        (void)hipGetLastError();  // an unrecorded pair is not an error
+        if (nar > ar_per_iter_) ar_per_iter_ = nar;
         acc_it_ += it;
         acc_m3_ += m3;
         acc_k5_ += k5;
@@ -1129,14 +1148,20 @@ void Session::sync(int* done, int* stopped) {
 
 void Session::mark(int slot) {
     if (!timing_) return;
-    hipEvent_t e = ev_[ev_.size() - 6 + slot];
+    hipEvent_t e = ev_[ev_.size() - EV_SLOTS + slot];
     if (e) TRITD_HIP(hipEventRecord(e, st_));
 }
 
 void Session::set_timing(int level) {
     timing_ = level;
-    acc_k5_ = acc_m3_ = acc_it_ = 0;
-    acc_n_ = 0;
+    acc_k5_ = acc_m3_ = acc_it_ = acc_ar_ = 0;
+    acc_n_ = ar_per_iter_ = 0;
+}
+
+void Session::comm_ms(double* allreduce_ms, int* per_iter) {
+    const double n = acc_n_ ? (double)acc_n_ : 1.0;
+    if (allreduce_ms) *allreduce_ms = acc_ar_ / n;
+    if (per_iter) *per_iter = ar_per_iter_;
 }
 
 void Session::kernel_ms(double* k5, double* m3, double* it, int* samples) {

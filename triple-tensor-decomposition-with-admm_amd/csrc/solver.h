@@ -94,6 +94,10 @@ class Session {
     bool dense_e() const { return de_; }
     void set_timing(int level);  // 0 off, TRITD_TIMING_ALL, TRITD_TIMING_K5
     void kernel_ms(double* k5, double* m3, double* it, int* samples);
+    // per timed iteration (TRITD_TIMING_ALL, with a communicator): ms inside
+    // the iteration's all-reduces (issue to completion on the session stream,
+    // so it includes waiting for the slowest rank) and their count
+    void comm_ms(double* allreduce_ms, int* per_iter);
     const std::vector<double>& probe_ms() const { return probe_ms_; }
     int probe_pick() const { return probe_pick_; }
 
@@ -240,10 +244,15 @@ class Session {
 
     int timing_ = 0;
     void mark(int slot);  // record timing event `slot` of this iteration (if it exists)
-    std::vector<hipEvent_t> ev_;  // per timed iteration: 6 events
+    // per timed iteration: EV_SLOTS events — 0 start, 1/2 K2, 3/4 K5, 5 end,
+    // then a (before, after) pair per all-reduce of the iteration
+    static constexpr int EV_AR = 4;  // all-reduce pairs timed per iteration
+    static constexpr int EV_SLOTS = 6 + 2 * EV_AR;
+    std::vector<hipEvent_t> ev_;
     std::vector<int> ev_iter_;
-    double acc_k5_ = 0, acc_m3_ = 0, acc_it_ = 0;
-    int acc_n_ = 0;
+    int ar_in_iter_ = 0;  // all-reduces issued so far in the current iteration
+    double acc_k5_ = 0, acc_m3_ = 0, acc_it_ = 0, acc_ar_ = 0;
+    int acc_n_ = 0, ar_per_iter_ = 0;
     void harvest_timing();
 };
 

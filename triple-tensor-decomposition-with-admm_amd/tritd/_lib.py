@@ -83,6 +83,7 @@ SIGNATURES = {
     "tritd_session_rre_parts_f32": (C.c_int, [vp, vp, i64, dp, dp]),
     "tritd_session_set_timing": (C.c_int, [vp, i32]),
     "tritd_session_kernel_ms": (C.c_int, [vp, dp, dp, dp, C.POINTER(i32)]),
+    "tritd_session_comm_ms": (C.c_int, [vp, dp, C.POINTER(i32)]),
     "tritd_session_probe": (C.c_int, [vp, dp, i32, C.POINTER(i32), C.POINTER(i32)]),
     "tritd_session_counters": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64)]),
     "tritd_session_k5_profile": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32)]),

@@ -461,6 +461,13 @@ class Session:
         check(fn(self._s, C.c_void_p(int(dX_ptr)), int(ldX), C.byref(num), C.byref(den)))
         return num.value, den.value
 
+    def comm_ms(self):
+        """(mean all-reduce ms per timed iteration, all-reduces per iteration)
+        — set_timing(True) with a communicator (tritd_session_comm_ms)."""
+        ms, n = C.c_double(0), _lib.i32(0)
+        check(lib.tritd_session_comm_ms(self._s, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     def probe(self):
         """(probe ms of each candidate tensor pool, index kept)"""
         cap = 64  # up to three rounds of candidates (solver.cpp probe_pool)

@@ -76,6 +76,58 @@ def low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123, mod
     return dict(D=D, Lstar=Lstar, A0=A0, B0=B0, C0=C0)
 
 
+def low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123, chunk=64):
+    """low_rank_plus_outliers(...) rounded to single (D and L* as float32,
+    column-major) without its fp64 full-size temporaries: the same draws from
+    the same generator streams, produced in chunks of mode-1 rows (the support
+    and value draws are C-ordered with i slowest, so row chunks consume them
+    in order; the value stream starts n1*n2*n3 draws later, where the
+    one-shot recipe's second call starts).  Equal to
+    `low_rank_plus_outliers(...)["D"].astype(np.float32)` except where
+    sigma = std(L*), summed chunk-wise here, differs in its last fp64 bit
+    (config 5: 2048x2048x256 in ~10 GB instead of ~35 GB)."""
+    import copy
+    rng = np.random.default_rng(seed)
+    As = np.asfortranarray(rng.standard_normal((n1, r, r)))
+    Bs = np.asfortranarray(rng.standard_normal((r, n2, r)))
+    Cs = np.asfortranarray(rng.standard_normal((r, r, n3)))
+    Ah, Bh, Ch = hat_factors(As, Bs, Cs)
+    R = Ah.shape[1]
+    KR = (Bh[:, None, :] * Ch[None, :, :]).reshape((n2 * n3, R), order="F")
+    L = np.empty((n1, n2, n3), dtype=np.float32, order="F")
+    # std(L*) in one pass: per-chunk mean and centred sum of squares,
+    # combined pairwise (Chan, Golub & LeVeque)
+    cnt, mean, m2 = 0, 0.0, 0.0
+    for i0 in range(0, n1, chunk):
+        i1 = min(n1, i0 + chunk)
+        blk = (Ah[i0:i1] @ KR.T).reshape((i1 - i0, n2, n3), order="F")
+        nb = blk.size
+        mb = float(blk.mean())
+        m2b = float(np.square(blk - mb).sum())
+        delta = mb - mean
+        tot = cnt + nb
+        mean += delta * nb / tot
+        m2 += m2b + delta * delta * cnt * nb / tot
+        cnt = tot
+        L[i0:i1] = blk
+    sigma = float(np.sqrt(m2 / cnt))
+    N = n1 * n2 * n3
+    rs = rng
+    bg = copy.deepcopy(rng.bit_generator)
+    bg.advance(N)
+    rv = np.random.Generator(bg)
+    D = np.empty((n1, n2, n3), dtype=np.float32, order="F")
+    for i0 in range(0, n1, chunk):
+        i1 = min(n1, i0 + chunk)
+        c = i1 - i0
+        sup = rs.random((c, n2, n3)) < p_out
+        vals = rv.uniform(-10.0 * sigma, 10.0 * sigma, size=(c, n2, n3))
+        blk = (Ah[i0:i1] @ KR.T).reshape((c, n2, n3), order="F")
+        D[i0:i1] = blk + np.where(sup, vals, 0.0)
+    A0, B0, C0 = random_factors(n1, n2, n3, r, init_seed)
+    return dict(D=D, Lstar=L, A0=A0, B0=B0, C0=C0)
+
+
 def sensor_like(n1=54, n2=4, n3=1152, r=5, missing=0.10, seed=0, init_seed=123):
     """Config 2 stand-in: smooth daily-periodic readings + noise, a seeded
     fraction zeroed (traffic_triple_comparison.m:27-35 zeroes missing entries)."""
