@@ -48,12 +48,18 @@ WORKLOADS = {
 
 
 def ensure_built():
-    """Rebuild libtritd.so when any source or header is newer than it (make's
-    own dependency check), so a stale library is never benchmarked as HEAD."""
+    """Rebuild libtritd.so when any source or header is newer than it, so a
+    stale library is never benchmarked as HEAD.  (Compared with the sources
+    themselves, not make's objects: a tree copied to a GPU box carries the
+    library but not csrc/build/, and must not recompile there.)"""
+    import glob
     csrc = os.path.join(PKG, "csrc")
-    if subprocess.run(["make", "-q", "-C", csrc], stdout=subprocess.DEVNULL,
-                      stderr=subprocess.DEVNULL).returncode != 0:
-        subprocess.run(["make", "-j8", "-C", csrc], check=True, stdout=subprocess.DEVNULL)
+    so = os.path.join(PKG, "tritd", "libtritd.so")
+    srcs = [f for e in ("*.hip", "*.cpp", "*.h", "Makefile") for f in glob.glob(os.path.join(csrc, e))]
+    srcs.append(os.path.join(ROOT, "include", "tritd.h"))
+    if os.path.exists(so) and all(os.path.getmtime(f) <= os.path.getmtime(so) for f in srcs):
+        return
+    subprocess.run(["make", "-j8", "-C", csrc], check=True, stdout=subprocess.DEVNULL)
 
 
 def cpu_baseline(D, r, opts, A0, B0, C0, iters):

@@ -710,7 +710,11 @@ template <int RP>
 __global__ __launch_bounds__(RP * 16) void k_solve_ns(const double* __restrict__ P,
                                                      const double* __restrict__ Q, int R,
                                                      double alpha, double* Ginv, int* flags,
-                                                     const int* stop) {
+                                                     const int* stop, FinishArgs fin) {
+    if (fin.on) {  // the previous iteration's finish first (launch_solve)
+        reduce_finish_wg<RP * 16>(fin);
+        __syncthreads();
+    }
     if (*stop) return;
     __builtin_amdgcn_s_setprio(3);  // beside K2 / K5 on the side stream: win issue
     constexpr int NWV = RP / 4, NT = RP / 16, LD = RP + 1, KS = RP / 4, RW = 4;
@@ -1084,12 +1088,17 @@ static unsigned mw_epoch() {
 // per-pivot sweep as fallback (k_solve_ns); RP = 128 / 256: the multi-
 // workgroup blocked sweep (k_solve_mw).
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
-                  int* flags, const int* stop, hipStream_t st) {
+                  int* flags, const int* stop, hipStream_t st, const FinishArgs* fin) {
+    FinishArgs f;  // on = 0: no finish
+    if (fin) {
+        if (RP > 64) throw Error(TRITD_ERR_ARG, "solve with a finish: RP <= 64 only");
+        f = *fin;
+    }
     switch (RP) {
 #define NS_CASE(RPV)                                                                            \
     case RPV:                                                                                   \
         hipLaunchKernelGGL(k_solve_ns<RPV>, dim3(1), dim3(RPV * 16), 0, st, P, Q, R, alpha, Ginv, \
-                           flags, stop);                                                        \
+                           flags, stop, f);                                                     \
         break;
         NS_CASE(16)
         NS_CASE(32)

@@ -33,6 +33,9 @@ struct SideSolve {
     double* gram_to = nullptr;
     int64_t gram_rows = 0;
     int gram_which = 0;
+    // 0: the Gram only, no solve (a sharded session's A^T A, formed beside
+    // M2 for the all-reduce that follows it)
+    int solve = 1;
 };
 
 // The reduction + stop test of one iteration's K5 norm pairs, run by an
@@ -139,8 +142,11 @@ inline size_t ginv_count(int RP) { return (size_t)ginv_sync(RP) + 16; }
 // Ginv = inv(P o Q + alpha I) on the leading R x R block (zero elsewhere),
 // plus the pinv request of pinv.h.  flags is unused by the solves since the
 // pinv fallback raises TRITD_FLAG_PINV_TOL itself (kept for the call shape).
+// fin.on (RP <= 64): the same launch first runs the norm reduction + stop
+// test of the previous iteration (finish.h) — a sharded session's finish and
+// update_B's solve both follow the first all-reduce, one launch for the two.
 void launch_solve(int RP, int R, const double* P, const double* Q, double alpha, double* Ginv,
-                  int* flags, const int* stop, hipStream_t st);
+                  int* flags, const int* stop, hipStream_t st, const FinishArgs* fin = nullptr);
 // Y = M * Ginv ([rows][RP]); optional transposed copy YT[k*ldT + i].  A set
 // request word makes every workgroup use pinv(saved Gram) instead (pinv.h);
 // flags[0] is raised when that pinv drops a singular value.

@@ -16,6 +16,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -165,7 +166,28 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         // compact E: 256 B per tile in either data type (before probing: the probe streams it)
         CE_.alloc_bytes((size_t)(g_.Ntm / 256) * 256);
         if (dy_) CE2_.alloc_bytes((size_t)(g_.Ntm / 256) * 256);
-        pool_.p = probe_pool(pool_bytes, slot, stagger);
+        // a host D is copied into a column-major staging buffer while the
+        // placement probe runs (its kernels and the copy engine overlap), then
+        // converted into the chosen pool below
+        std::function<void()> upload;
+        if (!(flags & TRITD_SESSION_D_ON_DEVICE) && g_.n1l > 0 && n2 * n3 > 0) {
+            upload = [&] {
+                dstage_.alloc_bytes((size_t)(g_.n1l * n2 * n3) * es_);
+                hipStream_t cs = nullptr;
+                TRITD_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+                hipError_t e;
+                if (ldD == g_.n1l)  // contiguous shard: one 1-D copy
+                    e = hipMemcpyAsync(dstage_.p, D, (size_t)(g_.n1l * n2 * n3) * es_,
+                                       hipMemcpyHostToDevice, cs);
+                else
+                    e = hipMemcpy2DAsync(dstage_.p, g_.n1l * es_, D, ldD * es_, g_.n1l * es_,
+                                         (size_t)(n2 * n3), hipMemcpyHostToDevice, cs);
+                if (e == hipSuccess) e = hipStreamSynchronize(cs);
+                (void)hipStreamDestroy(cs);
+                TRITD_HIP(e);
+            };
+        }
+        pool_.p = probe_pool(pool_bytes, slot, stagger, upload);
         TRITD_HIP(hipMemsetAsync(CE_.p, 0, CE_.bytes(), st_));
         if (dy_) TRITD_HIP(hipMemsetAsync(CE2_.p, 0, CE2_.bytes(), st_));
         pool_.n = pool_bytes / sizeof(double);
@@ -237,17 +259,10 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
         };
         if (flags & TRITD_SESSION_D_ON_DEVICE) {
             to_tm(D, ldD);
-        } else {
-            DBuf tmp;
-            tmp.alloc_bytes((size_t)(g_.n1l * n2 * n3) * es_);
-            if (ldD == g_.n1l)  // contiguous shard: one 1-D copy
-                TRITD_HIP(hipMemcpyAsync(tmp.p, D, (size_t)(g_.n1l * n2 * n3) * es_,
-                                         hipMemcpyHostToDevice, st_));
-            else
-                TRITD_HIP(hipMemcpy2DAsync(tmp.p, g_.n1l * es_, D, ldD * es_, g_.n1l * es_,
-                                           (size_t)(n2 * n3), hipMemcpyHostToDevice, st_));
-            to_tm(tmp.p, g_.n1l);
+        } else {  // staged during the placement probe (above)
+            to_tm(dstage_.p, g_.n1l);
             TRITD_HIP(hipStreamSynchronize(st_));
+            dstage_.release();
         }
     }
     upload_factors(A0, B0, C0);
@@ -416,11 +431,12 @@ void Session::do_m3_qi() {
 }
 
 void Session::solve(int mode, const double* P, const double* Q, double alpha, double* out,
-                    hipStream_t s) {
+                    hipStream_t s, const FinishArgs* fin) {
     if (!qi_) {
-        launch_solve(g_.RP, g_.R, P, Q, alpha, out, ctrl_ + 2, ctrl_, s);
+        launch_solve(g_.RP, g_.R, P, Q, alpha, out, ctrl_ + 2, ctrl_, s, fin);
         return;
     }
+    if (fin) throw Error(TRITD_ERR_ARG, "solve with a finish: CP model only");
     double* G = (mode == 0 ? GqA_ : mode == 1 ? GqB_ : GqC_).p;
     launch_qi_gram(g_.RP, g_.r, mode, P, Q, G, ctrl_, s);
     launch_solve(g_.RP, g_.R, G, ones_.p, alpha, out, ctrl_ + 2, ctrl_, s);
@@ -470,8 +486,10 @@ bool Session::small_ag(int64_t rows) const {
 // Small factors (rows*RP^2 <= 327 680): with defer (the fused single-GPU
 // schedule, side_gram_ok) the apply alone, the Gram left to the side solve
 // that next reads it (SideSolve::gram_rows), else apply + Gram in one
-// single-workgroup launch.  Larger factors: an apply and a Gram launch (a
-// side-job Gram of 512 x 64 outlasts M2: config 4 1.34 -> 1.41 ms).
+// single-workgroup launch.  Larger factors: an apply and a Gram launch for
+// A (a side-job Gram of 512 x 64 outlasts M2: config 4 1.34 -> 1.41 ms);
+// B and C, whose Grams ride beside K2 and K5 (hundreds of microseconds),
+// defer at any size (apply_gram_B / _C with defer_any).
 // Returns whether the Gram was left to the side solve.
 bool Session::apply_gram_A(double* AtA, bool defer) {
     if (defer && small_ag(g_.n1p)) {
@@ -488,7 +506,7 @@ bool Session::apply_gram_A(double* AtA, bool defer) {
 }
 
 bool Session::apply_gram_B(const double* M2, bool defer) {
-    if (defer && small_ag(g_.n2)) {
+    if (defer) {  // the Gram rides beside K2 (side solve C)
         do_apply_B(M2, GinvB_.p);
         return true;
     }
@@ -502,7 +520,7 @@ bool Session::apply_gram_B(const double* M2, bool defer) {
 }
 
 bool Session::apply_gram_C(bool defer) {
-    if (defer && small_ag(g_.n3p)) {
+    if (defer) {  // the Gram rides beside K5 (side solve A of k+1)
         do_apply_C(GinvC_.p);
         return true;
     }
@@ -516,10 +534,20 @@ bool Session::apply_gram_C(bool defer) {
     return false;
 }
 
-// the Grams can ride in side solves on the fused schedule with one GPU (with
-// a communicator A^TA is all-reduced with M2 before update_B's solve)
+// the Grams can ride in side solves on the fused schedule: A's on one GPU
+// only (with a communicator A^TA is all-reduced with M2 before update_B's
+// solve: it is formed by a gram-only side job of M2 instead), B's and C's in
+// either case (replicated factors)
 bool Session::side_gram_ok() const {
-    return !f32_ && !qi_ && g_.RP <= 64 && !(comm_ && comm_->active());
+    return side_gram_bc_ok() && !(comm_ && comm_->active());
+}
+
+bool Session::side_gram_bc_ok() const { return !f32_ && !qi_ && g_.RP <= 64; }
+
+// a sharded session's A^T A as a gram-only side job of M2: for shards of up
+// to 256 rows (the side Gram's MFMA loop then ends inside M2's time)
+bool Session::gram_a_in_m2() const {
+    return side_gram_bc_ok() && comm_ && comm_->active() && g_.n1p <= 256;
 }
 
 // side solve `s` first forms operand `which` (0 = P, 1 = Q) as X^T X into `to`
@@ -767,9 +795,15 @@ void Session::phaseC(int k) {
 // since a 100-iteration solve loses more to the probe than K5 gains
 // (bench.py end_to_end: +17 ms at config 4, +5.7 s at config 5, round 5).
 // TRITD_PROBE=n overrides either way (1 = off).
-double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
+double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger,
+                            std::function<void()> overlap) {
     const char* pe = std::getenv("TRITD_PROBE");
-    int want = pe ? std::atoi(pe) : (probe_ ? 8 : 1);
+    // a session asked to probe (TRITD_SESSION_PROBE) tries 8 candidates; so
+    // does one whose D comes from the host (the one-shot drop-in): its probe
+    // kernels run while the host copy of D is in flight (`overlap`), where
+    // they cost little; a device-resident D without the flag takes the first
+    // allocation
+    int want = pe ? std::atoi(pe) : ((probe_ || overlap) ? 8 : 1);
     // (small pools too: a mode-1 shard of 64 rows at 512^3 is a 0.8 GB pool, and
     // the slowest of P ranks sets the sharded iteration)
     if (pool_bytes < ((size_t)128 << 20)) want = 1;
@@ -780,7 +814,8 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     // round (a second one-class round is taken as that box's only class: with
     // one third of the pools fast, sixteen slow ones in a row are rare).
     // Earlier rounds stay allocated while the next one is drawn, so it gets
-    // new pages.
+    // new pages.  Why a placement matters and why no layout removes it:
+    // DESIGN.md §3 (profiles/round5/placement_strategies.txt).
     constexpr int rounds = 2;
     // keep room for the chosen pool, the other session buffers and 4 GiB
     const size_t reserve = pool_bytes / 2 + ((size_t)4 << 30);
@@ -807,31 +842,42 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
     probe_ms_.clear();
     size_t best = 0;
     if (want > 1 && cand.size() > 1) {
-        hipEvent_t e0, e1;
-        TRITD_HIP(hipEventCreate(&e0));
-        TRITD_HIP(hipEventCreate(&e1));
-        auto probe_from = [&](size_t from) {
+        // candidate c: a warm launch, then REPS launches each between events
+        constexpr int REPS = 2;
+        std::vector<hipEvent_t> ev;
+        auto probe_on = [&](size_t c) {
+            char* f[6];
+            for (int q = 0; q < 6; ++q) f[q] = reinterpret_cast<char*>(cand[c]) + q * slot + q * stagger;
+            // pool order: D, O, E, YL, YO, T
+            if (f32_)
+                launch_pool_probe32(g_, (float*)f[0], (float*)f[3], (float*)f[4], (float*)f[5], CE_.f(), st_);
+            else
+                launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[5], CE_.p, st_);
+        };
+        // enqueue every candidate of [from, end) without waiting
+        auto enqueue_from = [&](size_t from) {
             for (size_t c = from; c < cand.size(); ++c) {
-                char* f[6];
-                for (int q = 0; q < 6; ++q) f[q] = reinterpret_cast<char*>(cand[c]) + q * slot + q * stagger;
-                // pool order: D, O, E, YL, YO, T
-                auto probe = [&] {
-                    if (f32_)
-                        launch_pool_probe32(g_, (float*)f[0], (float*)f[3], (float*)f[4], (float*)f[5],
-                                            CE_.f(), st_);
-                    else
-                        launch_pool_probe(g_, (double*)f[0], (double*)f[3], (double*)f[5],
-                                          CE_.p, st_);
-                };
-                probe();  // warm
-                float ms = 1e30f;
-                for (int r = 0; r < 2; ++r) {
+                probe_on(c);  // warm
+                for (int r = 0; r < REPS; ++r) {
+                    hipEvent_t e0, e1;
+                    TRITD_HIP(hipEventCreate(&e0));
+                    TRITD_HIP(hipEventCreate(&e1));
+                    ev.push_back(e0);
+                    ev.push_back(e1);
                     TRITD_HIP(hipEventRecord(e0, st_));
-                    probe();
+                    probe_on(c);
                     TRITD_HIP(hipEventRecord(e1, st_));
-                    TRITD_HIP(hipEventSynchronize(e1));
+                }
+            }
+        };
+        auto collect_from = [&](size_t from) {
+            for (size_t c = from; c < cand.size(); ++c) {
+                float ms = 1e30f;
+                for (int r = 0; r < REPS; ++r) {
+                    const size_t q = 2 * (c * REPS + r);
+                    TRITD_HIP(hipEventSynchronize(ev[q + 1]));
                     float x = 0.f;
-                    TRITD_HIP(hipEventElapsedTime(&x, e0, e1));
+                    TRITD_HIP(hipEventElapsedTime(&x, ev[q], ev[q + 1]));
                     ms = std::fmin(ms, x);
                 }
                 probe_ms_.push_back(ms);
@@ -843,18 +889,24 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger) {
             const auto mm = std::minmax_element(probe_ms_.begin(), probe_ms_.end());
             return *mm.first < 0.92 * *mm.second;
         };
-        probe_from(0);
+        enqueue_from(0);
+        if (overlap) {  // the host copy of D runs while the probes do
+            overlap();
+            overlap = nullptr;
+        }
+        collect_from(0);
         for (int r = 1; r < rounds && !clearly_fast(); ++r) {
             const size_t from = cand.size();
             alloc_round(want);
             if (cand.size() == from) break;
-            probe_from(from);
+            enqueue_from(from);
+            collect_from(from);
         }
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     } else {
         probe_ms_.assign(cand.size(), 0.0);
     }
+    if (overlap) overlap();  // (no probe ran)
     for (size_t c = 0; c < cand.size(); ++c)
         if (c != best) (void)hipFree(cand[c]);
     probe_pick_ = (int)best;
@@ -935,24 +987,38 @@ void Session::iterate_fused(int k) {
     double* M2 = red1_.p;
     double* AtA = red1_.p + g_.n2 * RP;
     std::unique_ptr<Range> ph(new Range("update_A (:73-81)"));
-    const bool defer = side_gram_ok();
+    const bool defer = side_gram_ok(), defer_bc = side_gram_bc_ok();
+    const bool ga_m2 = gram_a_in_m2();
     do_m1();
-    const bool gA = apply_gram_A(AtA, defer);
+    const bool gA = ga_m2 ? (do_apply_A(GinvA_.p), false) : apply_gram_A(AtA, defer);
     ph.reset(new Range("update_B (:83-88)"));
     if (comm_ && comm_->active()) {
-        do_m2(M2);
+        if (ga_m2) {  // A^T A beside M2, for the all-reduce below
+            SideSolve sg;
+            sg.on = 1;
+            sg.solve = 0;
+            sg.R = g_.R;
+            with_gram(sg, Ah_.p, g_.n1p, AtA, 0);
+            launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_, sg);
+        } else {
+            do_m2(M2);
+        }
         // M1 .. M2 above ran before the stop test of iteration k-1: they
         // write only scratch and this iteration's A^ parity buffer.  The
         // all-reduce carries K5(k-1)'s norm partials; the finish of k-1
         // follows it, and every kernel after that checks its stop flag.
         const bool pend = norms_pending_;
         allreduce(red1_.p, red1_count() + (pend ? 2 * (int64_t)k5tail_ : 0));
+        // the finish of k-1 and update_B's solve in one launch (the finish
+        // runs first; the apply of B after it sees its stop flag)
+        FinishArgs f;
         if (pend) {
-            launch_reduce_finish(red1_.p + red1_count(), k5tail_, normD_, pend_k_, o_.tol,
-                                 errHist_.p, errL_.p, errO_.p, ctrl_, f32_, st_, /*clear=*/true);
+            f.p = red1_.p + red1_count(); f.n = k5tail_; f.normD = normD_; f.k = pend_k_;
+            f.tol = o_.tol; f.errHist = errHist_.p; f.errL = errL_.p; f.errO = errO_.p;
+            f.ctrl = ctrl_; f.single = (int)f32_; f.clear = 1; f.on = 1;
             norms_pending_ = false;
         }
-        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_);
+        solve(1, AtA, CtC_.p, o_.lambda2, GinvB_.p, st_, pend ? &f : nullptr);
     } else {
         // update_B's solve (A^TA of this iteration, C^TC) beside M2
         SideSolve sb;
@@ -961,7 +1027,7 @@ void Session::iterate_fused(int k) {
         if (gA) with_gram(sb, Ah_.p, g_.n1p, AtA, 0);
         launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_, sb);
     }
-    const bool gB = apply_gram_B(M2, defer);
+    const bool gB = apply_gram_B(M2, defer_bc);
     ph.reset(new Range("update_C (:90-95)"));
     mark(1);
     SideSolve sc;  // update_C's solve (:93 ridge) beside K2
@@ -971,7 +1037,7 @@ void Session::iterate_fused(int k) {
     launch_m3(g_, T_.p, Ah_.p, Bh_.p, m3part_.p, red2_.p, ctrl_, st_, 0, -1, sc);
     mark(2);
     allreduce(red2_.p, red2_count());
-    const bool gC = apply_gram_C(defer);
+    const bool gC = apply_gram_C(defer_bc);
     // the next update_A's solve (B^TB, C^TC of this iteration) beside K5
     ph.reset(new Range("fused update K5 (:38-59, :33)"));
     k5side_.P = BtB_.p; k5side_.Q = CtC_.p; k5side_.alpha = o_.lambda2; k5side_.Ginv = GinvA_.p;

@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <functional>
 #include <vector>
 
 #include "kernels.h"
@@ -52,6 +53,11 @@ struct DBuf {
         TRITD_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(double)));
     }
     void alloc_bytes(size_t bytes) { alloc((bytes + sizeof(double) - 1) / sizeof(double)); }
+    void release() {
+        if (p && owned) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
     float* f() const { return reinterpret_cast<float*>(p); }
     size_t bytes() const { return n * sizeof(double); }
 };
@@ -157,12 +163,18 @@ class Session {
     bool apply_gram_B(const double* M2, bool defer = false);
     bool apply_gram_C(bool defer = false);
     bool side_gram_ok() const;
+    bool side_gram_bc_ok() const;
+    bool gram_a_in_m2() const;
     bool overlap_ = false;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
     hipEvent_t evSA_ = nullptr, evSB_ = nullptr, evSC_ = nullptr;
     DBuf GinvA_, GinvB_, GinvC_;
-    double* probe_pool(size_t pool_bytes, size_t slot, size_t stagger);
+    // candidate pools timed with K5's access pattern; `overlap` (the host
+    // copy of D) runs while the probe kernels do
+    double* probe_pool(size_t pool_bytes, size_t slot, size_t stagger,
+                       std::function<void()> overlap);
+    DBuf dstage_;  // column-major staging of a host D (creation only)
     std::vector<double> probe_ms_;  // probe time of each candidate pool (ms)
     int probe_pick_ = 0;
     void upload_factors(const double* A0, const double* B0, const double* C0);
@@ -231,7 +243,7 @@ class Session {
     DBuf H_, ones_, GqA_, GqB_, GqC_;
     // inv(design Gram + alpha I) of update_A (mode 0), _B (1), _C (2)
     void solve(int mode, const double* P, const double* Q, double alpha, double* out,
-               hipStream_t s);
+               hipStream_t s, const FinishArgs* fin = nullptr);
     DBuf red1_, red2_, red3_;
     DBuf k5part_, m3part_, sqpart_;
     DBuf errHist_, errL_, errO_;

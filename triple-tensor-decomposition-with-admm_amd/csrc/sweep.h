@@ -106,6 +106,7 @@ __device__ __forceinline__ void side_solve(const SideSolve& s, double* rowbuf, d
     const double* Q = s.Q;
     if (s.gram_rows > 0) {
         side_gram<RP, NW>(s.gram_src, s.gram_rows, s.gram_to);
+        if (!s.solve) return;
         __syncthreads();  // (workgroup scope: the Gram is read back below by other waves)
         if (s.gram_which == 0)
             P = s.gram_to;
