@@ -445,13 +445,9 @@ void k5_fused(K5Args a) {
             // (selects, not a branch, for a dense tile: a branch would cut the
             // basic block and keep the scheduler from interleaving the decode
             // with the L MFMAs)
-#ifdef K5X_NOCE  // diagnosis only (round 5): no compact-E decode
-            for (int w = 0; w < 4; ++w) ev[w] = evp[w] = 0.0 * cx.ce + 0.0 * cx.cep;
-#else
             dn = ce_decode(cx.ce, lane, img, ev);
             dp = ce_decode(cx.cep, lane, imgp, evp);
             dense_fix(tt, dn, dp, ev, evp);
-#endif
             if (pf) load_slot(tt + 2, cx);  // cx.ce and cx.cep were consumed above
         }
         double tr[4], En[4];
@@ -480,20 +476,8 @@ void k5_fused(K5Args a) {
         } else {
             // L^T(t, ij) of this t-tile: KS dependent MFMAs
             d4 lacc = {0.0, 0.0, 0.0, 0.0};
-#if defined(K5X_NOL)  // diagnosis only (round 5)
-            lacc = d4{kr[0], kr[1], kr[2], kr[3]};
-#elif defined(K5X_LSPLIT)
-            d4 lacc1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int s = 0; s < KS; s += 2) {
-                lacc = mfma4(opL(buf, s), kr[s], lacc);
-                lacc1 = mfma4(opL(buf, s + 1), kr[s + 1], lacc1);
-            }
-            lacc = lacc + lacc1;
-#else
 #pragma unroll
             for (int s = 0; s < KS; ++s) lacc = mfma4(opL(buf, s), kr[s], lacc);
-#endif
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 d2v YLn2;
@@ -542,12 +526,7 @@ void k5_fused(K5Args a) {
                 __builtin_nontemporal_store(d2v{En[2], En[3]}, Ep2 + o + 64);
                 ++ndense;
             } else {
-#ifdef K5X_NOCE
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, En[0] + En[1] + En[2] + En[3]),
-                                                      rCEp, lane < 32 ? (lane & 31) * 8 : OOB, (int)(tt * 1024), 0);
-#else
                 ce_encode(En, lane, cs, rCEp, (int)(tt * 1024), Ep2, o, ndense);
-#endif
             }
             keep[2] = d2v{En[0], En[1]};
             keep[3] = d2v{En[2], En[3]};
@@ -569,20 +548,16 @@ void k5_fused(K5Args a) {
         if (TRITD_STORE_KEEP) asm volatile("" ::"v"(keep[0]), "v"(keep[1]), "v"(keep[2]), "v"(keep[3]));
         // W^T(k, ij) += sum_t C^(t,k) T(t, ij): K-step r covers t = t0+4r+(l>>4);
         // the C/D register of T is directly the B operand
-#ifndef K5X_NOW  // diagnosis only (round 5): no W MFMAs
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int m = 0; m < MT; ++m)
                 wacc[m] = mfma4(opW(buf, r, m), tr[r], wacc[m]);
-#endif
         // T data live until here (past the W MFMAs)
         if (TRITD_STORE_KEEP) asm volatile("" ::"v"(keep[4]), "v"(keep[5]));
         // the slice SD t-tiles ahead into the buffer read SD t-tiles ago
         if (ps) stage_store(slice_buf(tt + SD - t0));
-#ifndef K5X_NOBAR  // diagnosis only (round 5): no slice barrier (wrong results)
         if (bar) __syncthreads();
-#endif
         // step boundary: the scheduler would otherwise hoist the next step's
         // work above the barrier
         __builtin_amdgcn_sched_barrier(0);

@@ -25,6 +25,7 @@
 namespace tritd {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
 static constexpr int K5W = 4;
 // Compact-E slot (fp32): words 0..49 the nonzero values in (w, l) order,
 // bytes CE32_IDX_BYTE + q (words 50..62) their tile positions 4 l + w (the f4
@@ -533,11 +534,21 @@ void k5_f32s(K5Args32 a) {
         // share an MFMA changes (the f32 sum of L is formed in another order).
         auto sig = [&](int s4) { return 4 * (s4 >> 2) + (((s4 & 3) - tg) & 3); };
         float kr[NKR];
+        // gathered after the walk's first loads are issued (below): the
+        // four consecutive k of each granule as two 16-byte loads per factor
+        auto gather_kr = [&] {
+            const d2v* ah = reinterpret_cast<const d2v*>(a.Ah + (active ? i : 0) * RP);
+            const d2v* bh = reinterpret_cast<const d2v*>(a.Bh + (active ? j : 0) * RP);
 #pragma unroll
-        for (int s = 0; s < NKR; ++s) {
-            const int k = tg * KS + h * KSH + 4 * sig(s >> 2) + (s & 3);
-            kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
-        }
+            for (int s4 = 0; s4 < NKR / 4; ++s4) {
+                const int k0 = (tg * KS + h * KSH + 4 * sig(s4)) >> 1;  // d2v index
+                const d2v a0 = ah[k0], a1 = ah[k0 + 1], b0 = bh[k0], b1 = bh[k0 + 1];
+                kr[4 * s4 + 0] = active ? (float)(a0[0] * b0[0]) : 0.0f;
+                kr[4 * s4 + 1] = active ? (float)(a0[1] * b0[1]) : 0.0f;
+                kr[4 * s4 + 2] = active ? (float)(a1[0] * b1[0]) : 0.0f;
+                kr[4 * s4 + 3] = active ? (float)(a1[1] * b1[1]) : 0.0f;
+            }
+        };
 #pragma unroll
         for (int m = 0; m < NWT; ++m) wacc[m] = f4{0.0f, 0.0f, 0.0f, 0.0f};
         // only the h = 0 wave of the pair loads the tile, decodes E and runs
@@ -654,11 +665,15 @@ void k5_f32s(K5Args32 a) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) xa.x[q] = xb.x[q] = f4{0.0f, 0.0f, 0.0f, 0.0f};
         xa.ed = xb.ed = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        // every first load in flight before the first wait: the slots, tile
+        // 0, slice 0 and the Khatri-Rao gather (round 5: the gather used to
+        // complete before tile 0's loads were issued)
         load_slot(0, xa.ce);
         load_slot(1, xb.ce);
         load(0, xa);
-        if (ce32_is_dense(xa.ce)) load_dense(0, xa);
         stage_load(0);
+        gather_kr();
+        if (ce32_is_dense(xa.ce)) load_dense(0, xa);
         stage_store(0);
         __syncthreads();
         int64_t tt = 0;
@@ -702,6 +717,9 @@ void k5_f32s(K5Args32 a) {
     // the pair's roles alternate between workgroups (the h = 0 wave carries
     // the elementwise chain; the two workgroups resident on a CU then put it
     // on different SIMDs, as far as waves map to SIMDs in order)
+    // (Walking pairs grid-stride in 512 persistent workgroups instead, to
+    // save the turnover of 131 072 short-lived ones: K5 15.88 vs 13.79 ms,
+    // profiles/round5/ab_c5_prologue_persistent.txt — dropped.)
     const int hrole = (wid & 1) ^ (int)(blockIdx.x & 1);
     if (hrole)
         walk(std::integral_constant<int, 1>{});

@@ -486,10 +486,10 @@ bool Session::small_ag(int64_t rows) const {
 // Small factors (rows*RP^2 <= 327 680): with defer (the fused single-GPU
 // schedule, side_gram_ok) the apply alone, the Gram left to the side solve
 // that next reads it (SideSolve::gram_rows), else apply + Gram in one
-// single-workgroup launch.  Larger factors: an apply and a Gram launch for
-// A (a side-job Gram of 512 x 64 outlasts M2: config 4 1.34 -> 1.41 ms);
-// B and C, whose Grams ride beside K2 and K5 (hundreds of microseconds),
-// defer at any size (apply_gram_B / _C with defer_any).
+// single-workgroup launch.  Larger factors: an apply and a Gram launch (a
+// side-job Gram of 512 x 64 outlasts M2: config 4 1.34 -> 1.41 ms; beside
+// K2 / K5 of a 64-row shard it doubled both, round 5, while at config 4 it
+// moved nothing beyond box noise: profiles/round5/shard8_deferred_grams.txt).
 // Returns whether the Gram was left to the side solve.
 bool Session::apply_gram_A(double* AtA, bool defer) {
     if (defer && small_ag(g_.n1p)) {
@@ -506,7 +506,7 @@ bool Session::apply_gram_A(double* AtA, bool defer) {
 }
 
 bool Session::apply_gram_B(const double* M2, bool defer) {
-    if (defer) {  // the Gram rides beside K2 (side solve C)
+    if (defer && small_ag(g_.n2)) {  // the Gram rides beside K2 (side solve C)
         do_apply_B(M2, GinvB_.p);
         return true;
     }
@@ -520,7 +520,7 @@ bool Session::apply_gram_B(const double* M2, bool defer) {
 }
 
 bool Session::apply_gram_C(bool defer) {
-    if (defer) {  // the Gram rides beside K5 (side solve A of k+1)
+    if (defer && small_ag(g_.n3p)) {  // the Gram rides beside K5 (side solve A of k+1)
         do_apply_C(GinvC_.p);
         return true;
     }
@@ -544,10 +544,11 @@ bool Session::side_gram_ok() const {
 
 bool Session::side_gram_bc_ok() const { return !f32_ && !qi_ && g_.RP <= 64; }
 
-// a sharded session's A^T A as a gram-only side job of M2: for shards of up
-// to 256 rows (the side Gram's MFMA loop then ends inside M2's time)
+// a sharded session's A^T A as a gram-only side job of M2: shards of up to
+// 64 rows (16 K-steps of the side Gram, which then ends inside M2's time;
+// its load round trips make 128+ rows outlast M2)
 bool Session::gram_a_in_m2() const {
-    return side_gram_bc_ok() && comm_ && comm_->active() && g_.n1p <= 256;
+    return side_gram_bc_ok() && comm_ && comm_->active() && g_.n1p <= 64;
 }
 
 // side solve `s` first forms operand `which` (0 = P, 1 = Q) as X^T X into `to`
@@ -798,12 +799,13 @@ void Session::phaseC(int k) {
 double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger,
                             std::function<void()> overlap) {
     const char* pe = std::getenv("TRITD_PROBE");
-    // a session asked to probe (TRITD_SESSION_PROBE) tries 8 candidates; so
-    // does one whose D comes from the host (the one-shot drop-in): its probe
-    // kernels run while the host copy of D is in flight (`overlap`), where
-    // they cost little; a device-resident D without the flag takes the first
-    // allocation
-    int want = pe ? std::atoi(pe) : ((probe_ || overlap) ? 8 : 1);
+    // a session asked to probe (TRITD_SESSION_PROBE) tries 8 candidates, with
+    // a host D copied in while the probe kernels run (`overlap`); without the
+    // flag the first allocation is kept: for a one-shot 100-iteration solve
+    // the candidate pools' allocation costs more than a fast placement saves
+    // (config 4: 250 vs 212 ms end to end, profiles/round5/bench_line.json;
+    // DESIGN.md §3)
+    int want = pe ? std::atoi(pe) : (probe_ ? 8 : 1);
     // (small pools too: a mode-1 shard of 64 rows at 512^3 is a 0.8 GB pool, and
     // the slowest of P ranks sets the sharded iteration)
     if (pool_bytes < ((size_t)128 << 20)) want = 1;
