@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build libtritd variants that differ only in the -D flags of k_admm.hip / k_contract.hip, into ab/<name>.so
+# Build libtritd variants that differ only in the -D flags of the kernel files (k_*.hip), into ab/<name>.so
 #   bash tools/build_k5_variants.sh name1="-DK5_EXP=1" name2="-DFOO=2" ...
 set -e
 cd "$(dirname "$0")/../triple-tensor-decomposition-with-admm_amd/csrc"
@@ -7,7 +7,7 @@ make -j8 >/dev/null
 mkdir -p ../../ab
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  rm -rf build_$name; cp -r build build_$name; rm -f build_$name/k_admm.o build_$name/k_admm32.o
+  rm -rf build_$name; cp -r build build_$name; rm -f build_$name/k_*.o
   make OBJDIR=build_$name OUT=../../ab/$name.so EXTRA="$flags" >/dev/null &
 done
 wait

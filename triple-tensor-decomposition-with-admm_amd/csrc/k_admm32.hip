@@ -430,12 +430,12 @@ void k5_f32(K5Args32 a) {
 // RP = 256 with the rank split over a wave pair (the default there): two
 // waves share each ij-tile, wave h of the pair holding the K-steps
 // s in [h*KS/2, (h+1)*KS/2) of the L operand (k = (l>>4) * KS + s) and the
-// W M-tiles m = 4q + u of granules q in [h*G/2, (h+1)*G/2).  Per t-tile each
-// forms its half of L, the pair adds the halves through LDS (both in the same
-// order: both waves then hold bitwise the same L), both run the elementwise
-// chain (wave 0 stores Y_L, Y_O, T, E and sums the norms), and each
-// accumulates its half of W.  Half the L operands and W accumulators per
-// wave fit two waves per SIMD, which the one-wave kernel (352 VGPRs) could
+// W M-tiles m = 4q + u of granules q in [0, GH0) (h = 0) or [GH0, G) (h = 1).
+// Per t-tile each forms its half of L, the pair adds the halves through LDS
+// (both in the same order: both waves then hold bitwise the same L), wave 0
+// runs the elementwise chain (stores Y_L, Y_O, T, E and sums the norms), and
+// each accumulates its W M-tiles.  Half the L operands and part of the W
+// accumulators per wave fit two waves per SIMD, which the one-wave kernel (352 VGPRs) could
 // not: at one wave per SIMD a t-tile step took ~8 800 cycles against ~5 200
 // of issue.
 template <int RP>
@@ -444,7 +444,12 @@ void k5_f32s(K5Args32 a) {
     static_assert(RP == 256, "k5_f32s: RP = 256 (the L-read permutation assumes 4 granules per group)");
     if (*a.stop) return;
     constexpr int KS = RP / 4, MT = RP / 16, LDC = RP + 4;
-    constexpr int G = MT / 4, GH = G / 2, KSH = KS / 2, MTH = MT / 2;
+    constexpr int G = MT / 4, KSH = KS / 2;
+    // W granules (of 4 M-tiles) of the h = 0 wave, which also runs the
+    // elementwise chain; h = 1 holds the other G - GH0 (round 5: 1 of 4 vs
+    // 2 of 4: K5 13.65 vs 13.75 ms; the L K-steps split 4:12 or 12:4 instead
+    // of 8:8: 14.00 / 14.02 ms — profiles/round5/ab_k5_split.txt)
+    constexpr int GH0 = 1;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int slot = wid >> 1;  // ij-tile of the pair within the workgroup
@@ -518,13 +523,14 @@ void k5_f32s(K5Args32 a) {
     unsigned ndense = 0;
     // (Splitting the pair by role instead — one wave all of L and the chain,
     // the other all of W — measured 16.03 vs 15.22 ms, round 3.)
-    f4 wacc[MTH];
 
     // the walk, specialised per half (straight-line code in each)
     auto walk = [&](auto HC) {
         constexpr int h = decltype(HC)::value;
         constexpr int NKR = KSH;  // KR operands this wave holds
-        constexpr int NWT = MTH;  // W M-tiles this wave accumulates
+        constexpr int NG = h ? G - GH0 : GH0;  // W granules of this wave
+        constexpr int NWT = 4 * NG;            // W M-tiles this wave accumulates
+        f4 wacc[NWT];
         // KR(ij = l & 15, k), single-rounded, for the k this lane's L read
         // takes at slot s = 4 s4 + u: granule s4 of its half, permuted within
         // each group of 4 granules by the lane's K group tg (sig below), so
@@ -555,9 +561,9 @@ void k5_f32s(K5Args32 a) {
         // the elementwise chain (round 3: K5 15.73 -> 15.45 ms); the h = 1
         // wave takes T from the LDS transpose buffer a step later
         constexpr bool CHAIN = h == 0;
-        // W^T += C^T T for this half's M-tiles (granules q in [h*GH, (h+1)*GH))
+        // W^T += C^T T for this wave's M-tiles (granules q in [Q0, Q0 + NG))
         auto wmfma = [&](const float* cR, const float (&tr)[4]) {
-            constexpr int NQ = NWT / 4, Q0 = h * GH;  // granules of this wave
+            constexpr int NQ = NG, Q0 = h ? GH0 : 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const f4* cW = reinterpret_cast<const f4*>(cR + (4 * tg + r) * LDC);
@@ -702,14 +708,14 @@ void k5_f32s(K5Args32 a) {
             }
         }
         // W^T C/D layout: M-tile m row rho = 4(l>>4) + rr, col ij = l & 15,
-        // k = rho * MT + m; this half's m = 4(h*GH + q) + u
+        // k = rho * MT + m; this wave's m = 4(Q0 + q) + u
         float* wl = &sC[0][0];  // the C^ slices are dead after the walk
         __syncthreads();
 #pragma unroll
         for (int mq = 0; mq < NWT; ++mq)
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-                const int m = 4 * h * GH + mq;
+                const int m = 4 * (h ? GH0 : 0) + mq;
                 const int k = (4 * tg + rr) * MT + m;
                 wl[slot * WS + k * 16 + il] = wacc[mq][rr];
             }

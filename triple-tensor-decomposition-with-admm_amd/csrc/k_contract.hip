@@ -646,12 +646,18 @@ __global__ __launch_bounds__(64 * NW) void k_gram(const double* __restrict__ X, 
     }
 }
 
+// side = true: four-wave workgroups, for a Gram on the side stream beside a
+// grid of 256-thread workgroups that fills the chip (K2 / K5): a 1024-thread
+// workgroup fits only where four of theirs retired on one CU at once, and
+// waited for the whole grid (config 5: Gram B 4.9 ms beside K2, solve C
+// after it on the critical path)
 void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop,
-                 hipStream_t st) {
-#ifndef TRITD_GRAM_NW
-#define TRITD_GRAM_NW 16
-#endif
-    hipLaunchKernelGGL(k_gram<TRITD_GRAM_NW>, dim3((RP / 16) * (RP / 16)), dim3(64 * TRITD_GRAM_NW), 0, st, X, rows, RP, G, stop);
+                 hipStream_t st, bool side) {
+    const dim3 grid((RP / 16) * (RP / 16));
+    if (side)
+        hipLaunchKernelGGL(k_gram<4>, grid, dim3(64 * 4), 0, st, X, rows, RP, G, stop);
+    else
+        hipLaunchKernelGGL(k_gram<16>, grid, dim3(64 * 16), 0, st, X, rows, RP, G, stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -1323,13 +1329,15 @@ void launch_apply_gram(int RP, const double* M, int64_t rows, const double* Ginv
 // the solve set the request word.  RP <= 64 works in LDS; 128 / 256 in the
 // Ginv buffer's scratch (the saved Gram is rotated in place, V beside it).
 // ---------------------------------------------------------------------------
+// (256 threads at every RP: the launch follows the solve on the side stream,
+// beside a K2 / K5 grid of 256-thread workgroups, and a 1024-thread one would
+// wait for that grid to drain; the fallback itself is rare)
 template <int RP>
-__global__ __launch_bounds__(RP <= 64 ? 256 : 1024) void k_pinv_fix(double* Ginv, const int* stop,
-                                                                    int* flags) {
+__global__ __launch_bounds__(256) void k_pinv_fix(double* Ginv, const int* stop, int* flags) {
     if (*stop) return;
     const double req = Ginv[ginv_req(RP)];
     if (req == 0.0) return;
-    constexpr int NT = RP <= 64 ? 256 : 1024;
+    constexpr int NT = 256;
     __shared__ double rot[RP], red[NT / 64 + RP];
     __shared__ int pq[RP];
     double* G = Ginv + (int64_t)RP * RP;
@@ -1349,7 +1357,7 @@ __global__ __launch_bounds__(RP <= 64 ? 256 : 1024) void k_pinv_fix(double* Ginv
 
 void launch_pinv_fix(int RP, double* Ginv, const int* stop, int* flags, hipStream_t st) {
 #define FIX_CASE(RPV) \
-    case RPV: hipLaunchKernelGGL(k_pinv_fix<RPV>, dim3(1), dim3(RPV <= 64 ? 256 : 1024), 0, st, Ginv, stop, flags); break;
+    case RPV: hipLaunchKernelGGL(k_pinv_fix<RPV>, dim3(1), dim3(256), 0, st, Ginv, stop, flags); break;
     switch (RP) {
         FIX_CASE(16)
         FIX_CASE(32)

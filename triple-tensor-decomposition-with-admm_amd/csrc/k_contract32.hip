@@ -6,6 +6,7 @@
 // (A^ o B^, B^, A^) are the double factors rounded to single, as MATLAB
 // converts the double design matrix F/G/H when it meets a single X_k.
 #include "kernels.h"
+#include "finish.h"
 
 namespace tritd {
 
@@ -131,11 +132,20 @@ __global__ __launch_bounds__(256) void k_m2_32v(const float* __restrict__ Wk,
 // the row k of A^T (n1p doubles, rounded to single once) is loaded once per
 // JB rows instead of once per row (k_m2_32v re-read all of A^T for every j:
 // 8.6 GB of L2 traffic beside the 4.3 GB of W at config 5).  n1p <= 64*4*UG.
+// The extra column of workgroups (fin.on): the previous iteration's norm
+// reduction and stop test in its first one, as k_m1 (k_contract.hip) — here
+// rather than in M1, whose 2 048 workgroups are one full round of the chip
+// (an extra one there lengthened M1 by ~60 us, config 5).  M1, apply A and
+// Gram A before it write only scratch and this iteration's A^ parity buffer.
 template <int UG, int JB>
 __global__ __launch_bounds__(256) void k_m2_32w(const float* __restrict__ Wk,
                                                 const double* __restrict__ AhT, double* M2,
                                                 int64_t n1p, int64_t n2, int64_t plane, int RP,
-                                                const int* stop) {
+                                                const int* stop, FinishArgs fin) {
+    if (fin.on && blockIdx.x == gridDim.x - 1) {
+        if (blockIdx.y == 0) reduce_finish_wg<256>(fin);
+        return;
+    }
     if (*stop) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = blockIdx.y;
@@ -182,14 +192,17 @@ __global__ __launch_bounds__(256) void k_m2_32w(const float* __restrict__ Wk,
 }
 
 void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
-                  hipStream_t st) {
+                  hipStream_t st, const FinishArgs& fin) {
     constexpr int UG = 8, JB = 8;
     if (g.n1p <= 64 * 4 * UG) {
-        hipLaunchKernelGGL((k_m2_32w<UG, JB>), dim3((unsigned)cdiv(g.n2, 4 * JB), (unsigned)g.RP),
-                           dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
+        hipLaunchKernelGGL((k_m2_32w<UG, JB>), dim3((unsigned)cdiv(g.n2, 4 * JB) + (fin.on ? 1 : 0), (unsigned)g.RP),
+                           dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop, fin);
         TRITD_CHECK_LAUNCH();
         return;
     }
+    if (fin.on)  // (n1p > 2048: the finish as its own launch, ahead of the contraction)
+        launch_reduce_finish(fin.p, fin.n, fin.normD, fin.k, fin.tol, fin.errHist, fin.errL, fin.errO,
+                             fin.ctrl, fin.single != 0, st, fin.clear != 0);
     hipLaunchKernelGGL(k_m2_32v, dim3((unsigned)g.n2, (unsigned)cdiv(g.RP, 4)), dim3(256), 0, st, Wk,
                        AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop);
     TRITD_CHECK_LAUNCH();
@@ -413,8 +426,8 @@ __global__ __launch_bounds__(256) void k_apply_mfma(const TM* __restrict__ M, in
 
 void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, double* Ginv,
                       double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
-                      int* flags, hipStream_t st) {
-    launch_pinv_fix(RP, Ginv, stop, flags, st);
+                      int* flags, hipStream_t st, bool fix) {
+    if (fix) launch_pinv_fix(RP, Ginv, stop, flags, st);
     {
         const int64_t tiles = cdiv(rows, 16) * (RP / 16);
         const dim3 grid((unsigned)cdiv(tiles, 4)), block(256);

@@ -127,7 +127,8 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
                double* M3, const int* stop, hipStream_t st, int64_t ahj = 0, int64_t bhj = -1,
                const SideSolve& side = SideSolve{});
 // G = X^T X over `rows` rows of a row-major [rows][RP] factor
-void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop, hipStream_t st);
+void launch_gram(int RP, const double* X, int64_t rows, double* G, const int* stop, hipStream_t st,
+                 bool side = false);
 // Ginv buffers, one per Gram slot (pinv.h): [0, RP^2) the inverse, read by
 // the apply; [RP^2, 2 RP^2) the Gram, saved by a solve whose pivot test came
 // near pinv's cutoff; [2 RP^2, 3 RP^2) eigenvector scratch of the RP > 64
@@ -289,18 +290,19 @@ void launch_widen(const float* x, int64_t n, double* y, hipStream_t st);
 void launch_m1_32(const Geom& g, const float* Wk, const double* Bh, float* M1, const int* stop,
                   hipStream_t st);
 void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2, const int* stop,
-                  hipStream_t st);
+                  hipStream_t st, const FinishArgs& fin = FinishArgs());
 int m3_parts32(const Geom& g);
 void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double* Bh, double* part,
                   double* M3, const int* stop, hipStream_t st);
 // Y = M * Ginv for any RP; M double or single (Mf); round32: results rounded to
 // single (then stored as double; MATLAB's (X*F')*pinv(G) is single for single
 // data); YT transposed copy, YF single copy (either may be null)
-// (the pinv fallback runs first, in k_pinv_fix: a one-workgroup launch that
-// returns at once unless the request word is set)
+// (fix: the pinv fallback runs first, in k_pinv_fix: a one-workgroup launch
+// that returns at once unless the request word is set; false when the caller
+// launched it behind the solve already)
 void launch_apply_gen(int RP, const double* M, const float* Mf, int64_t rows, double* Ginv,
                       double* Y, double* YT, int64_t ldT, float* YF, bool round32, const int* stop,
-                      int* flags, hipStream_t st);
+                      int* flags, hipStream_t st, bool fix = true);
 // the pinv fallback alone (pinv.h): Ginv[0, RP^2) <- pinv(saved Gram) if requested
 void launch_pinv_fix(int RP, double* Ginv, const int* stop, int* flags, hipStream_t st);
 

@@ -390,27 +390,30 @@ IterScalars32 Session::scalars32(int k) const {
 void Session::do_m1() {
     if (qi_)
         launch_m1_qi(g_, g_.r, Wk_.p, Bh_.p, M1_.p, ctrl_, st_);
-    else if (f32_)
+    else if (f32_)  // (its finish rides in M2: do_m2)
         launch_m1_32(g_, Wk_.f(), Bh_.p, M1_.f(), ctrl_, st_);
-    else {
-        // single GPU, fused schedule: the previous K5's norm reduction and
-        // stop test ride in an extra workgroup of this M1 (finish.h)
-        FinishArgs f;
-        if (norms_pending_ && !(comm_ && comm_->active())) {
-            f.p = k5part_.p; f.n = k5n(); f.normD = normD_; f.k = pend_k_; f.tol = o_.tol;
-            f.errHist = errHist_.p; f.errL = errL_.p; f.errO = errO_.p; f.ctrl = ctrl_;
-            f.single = (int)f32_; f.on = 1;
-            norms_pending_ = false;
-        }
-        launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_, f);
+    else  // the previous K5's norm reduction and stop test in an extra workgroup (finish.h)
+        launch_m1(g_, Wk_.p, Bh_.p, M1_.p, ctrl_, st_, take_finish());
+}
+
+// The pending norm reduction + stop test of the previous iteration (single
+// GPU: K5's own partials), for an extra workgroup of the next M1 / M2
+FinishArgs Session::take_finish() {
+    FinishArgs f;
+    if (norms_pending_ && !(comm_ && comm_->active())) {
+        f.p = k5part_.p; f.n = k5n(); f.normD = normD_; f.k = pend_k_; f.tol = o_.tol;
+        f.errHist = errHist_.p; f.errL = errL_.p; f.errO = errO_.p; f.ctrl = ctrl_;
+        f.single = (int)f32_; f.on = 1;
+        norms_pending_ = false;
     }
+    return f;
 }
 
 void Session::do_m2(double* M2) {
     if (qi_)
         launch_m2_qi(g_, g_.r, Wk_.p, AhT_.p, M2, ctrl_, st_);
     else if (f32_)
-        launch_m2_32(g_, Wk_.f(), AhT_.p, M2, ctrl_, st_);
+        launch_m2_32(g_, Wk_.f(), AhT_.p, M2, ctrl_, st_, take_finish());
     else
         launch_m2(g_, Wk_.p, AhT_.p, M2, ctrl_, st_);
 }
@@ -434,12 +437,15 @@ void Session::solve(int mode, const double* P, const double* Q, double alpha, do
                     hipStream_t s, const FinishArgs* fin) {
     if (!qi_) {
         launch_solve(g_.RP, g_.R, P, Q, alpha, out, ctrl_ + 2, ctrl_, s, fin);
-        return;
+    } else {
+        if (fin) throw Error(TRITD_ERR_ARG, "solve with a finish: CP model only");
+        double* G = (mode == 0 ? GqA_ : mode == 1 ? GqB_ : GqC_).p;
+        launch_qi_gram(g_.RP, g_.r, mode, P, Q, G, ctrl_, s);
+        launch_solve(g_.RP, g_.R, G, ones_.p, alpha, out, ctrl_ + 2, ctrl_, s);
     }
-    if (fin) throw Error(TRITD_ERR_ARG, "solve with a finish: CP model only");
-    double* G = (mode == 0 ? GqA_ : mode == 1 ? GqB_ : GqC_).p;
-    launch_qi_gram(g_.RP, g_.r, mode, P, Q, G, ctrl_, s);
-    launch_solve(g_.RP, g_.R, G, ones_.p, alpha, out, ctrl_ + 2, ctrl_, s);
+    // the generic apply's pinv fallback, on the solve's stream (a side-stream
+    // solve then hands over a finished Ginv: one launch fewer on the main one)
+    if (gen_apply()) launch_pinv_fix(g_.RP, out, ctrl_, ctrl_ + 2, s);
 }
 
 // (X*F')*pinv(G): fp64 path through the MFMA apply (RP <= 64); fp32
@@ -447,10 +453,10 @@ void Session::solve(int mode, const double* P, const double* Q, double alpha, do
 void Session::do_apply_A(double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, nullptr, M1_.f(), g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
-                         true, ctrl_, ctrl_ + 2, st_);
+                         true, ctrl_, ctrl_ + 2, st_, false);
     else if (g_.RP > 64)  // fp64 r = 9..16
         launch_apply_gen(g_.RP, M1_.p, nullptr, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
-                         false, ctrl_, ctrl_ + 2, st_);
+                         false, ctrl_, ctrl_ + 2, st_, false);
     else
         launch_apply(g_.RP, M1_.p, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, ctrl_, ctrl_ + 2, st_);
 }
@@ -458,10 +464,10 @@ void Session::do_apply_A(double* Ginv) {
 void Session::do_apply_B(const double* M2, double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, true, ctrl_, ctrl_ + 2,
-                         st_);
+                         st_, false);
     else if (g_.RP > 64)  // fp64 r = 9..16
         launch_apply_gen(g_.RP, M2, nullptr, g_.n2, Ginv, Bh_.p, nullptr, 0, nullptr, false, ctrl_, ctrl_ + 2,
-                         st_);
+                         st_, false);
     else
         launch_apply(g_.RP, M2, g_.n2, Ginv, Bh_.p, nullptr, 0, ctrl_, ctrl_ + 2, st_);
 }
@@ -469,10 +475,10 @@ void Session::do_apply_B(const double* M2, double* Ginv) {
 void Session::do_apply_C(double* Ginv) {
     if (f32_)
         launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ChF_.f(),
-                         true, ctrl_, ctrl_ + 2, st_);
+                         true, ctrl_, ctrl_ + 2, st_, false);
     else if (g_.RP > 64)  // fp64 r = 9..16
         launch_apply_gen(g_.RP, red2_.p, nullptr, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, nullptr,
-                         false, ctrl_, ctrl_ + 2, st_);
+                         false, ctrl_, ctrl_ + 2, st_, false);
     else
         launch_apply(g_.RP, red2_.p, g_.n3p, Ginv, Ch_.p, ChT_.p, g_.n3p, ctrl_, ctrl_ + 2, st_);
 }
@@ -962,7 +968,7 @@ void Session::iterate_overlapped(int k) {
     do_apply_B(M2, GinvB_.p);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
-    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_, true);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     mark(1);
@@ -972,10 +978,20 @@ void Session::iterate_overlapped(int k) {
     do_apply_C(GinvC_.p);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_, true);
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
-    launch_k5_full(k, /*fused_finish=*/true);
+    if (qi_) {
+        launch_k5_full(k, /*fused_finish=*/true);
+        return;
+    }
+    // the norm reduction and stop test of k ride in the next M1 (do_m1; fp32:
+    // M2, do_m2), or flush_norms when the loop ends first
+    mark(3);
+    launch_k5_any(k, /*prologue=*/false);
+    mark(4);
+    norms_pending_ = true;
+    pend_k_ = k;
 }
 
 // Single-stream iteration (fused_): every kernel on the main stream in
@@ -1088,7 +1104,7 @@ void Session::iterate_sharded(int k) {
     do_apply_B(M2, GinvB_.p);
     TRITD_HIP(hipEventRecord(evBtB_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evBtB_, 0));
-    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_);
+    launch_gram(RP, Bh_.p, g_.n2, BtB_.p, ctrl_, side_, true);
     solve(2, AtA, BtB_.p, 1e-9, GinvC_.p, side_);  // :93 ridge
     TRITD_HIP(hipEventRecord(evSC_, side_));
     mark(1);
@@ -1099,7 +1115,7 @@ void Session::iterate_sharded(int k) {
     do_apply_C(GinvC_.p);
     TRITD_HIP(hipEventRecord(evCtC_, st_));
     TRITD_HIP(hipStreamWaitEvent(side_, evCtC_, 0));
-    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_);
+    launch_gram(RP, Ch_.p, g_.n3p, CtC_.p, ctrl_, side_, true);
     solve(0, BtB_.p, CtC_.p, o_.lambda2, GinvA_.p, side_);
     TRITD_HIP(hipEventRecord(evSA_, side_));
     launch_k5_full(k, /*fused_finish=*/false);

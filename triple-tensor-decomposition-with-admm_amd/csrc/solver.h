@@ -165,6 +165,9 @@ class Session {
     bool side_gram_ok() const;
     bool side_gram_bc_ok() const;
     bool gram_a_in_m2() const;
+    // the applies take the generic kernel (launch_apply_gen): fp32, or RP > 64
+    bool gen_apply() const { return f32_ || g_.RP > 64; }
+    FinishArgs take_finish();
     bool overlap_ = false;
     hipStream_t side_ = nullptr;
     hipEvent_t evAtA_ = nullptr, evBtB_ = nullptr, evCtC_ = nullptr;
