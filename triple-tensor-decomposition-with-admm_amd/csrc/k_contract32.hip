@@ -314,30 +314,49 @@ __global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
         }
     }
     if (tact) {
-        // C/D (f32): row k = 16m + 4(l>>4) + rr, col t = 16 tt + (l & 15)
-        double* out = part + (q * jc + c) * n3p * RP;
+        // the slab in the accumulators' own order (f32, as summed: exact):
+        // f4 (tt*MT + m)*64 + lane, one 1 KB piece per store (k_m3_reduce32
+        // maps it back: C/D row k = 16m + 4(l>>4) + rr, col t = 16 tt + (l & 15))
+        f4* out = reinterpret_cast<f4*>(reinterpret_cast<float*>(part) + (q * jc + c) * n3p * RP);
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
-                out[(tt * 16 + il) * RP + 16 * m + 4 * tg + rr] = (double)acc[m][rr];
+        for (int m = 0; m < MT; ++m) out[(tt * MT + m) * 64 + lane] = acc[m];
     }
 }
 
-// M3[e] = single(sum over parts in fixed order), stored as double
-__global__ __launch_bounds__(256) void k_m3_reduce32(const double* __restrict__ part, double* M3,
-                                                     int64_t count, int nparts, const int* stop) {
+// M3 = single(sum over parts in fixed order), stored as double.  The parts
+// are f32 slabs in K2's accumulator order (element e: rr = e & 3, lane =
+// (e >> 2) & 63, m = (e >> 8) % MT, t-tile = (e >> 8) / MT) — half the bytes
+// of double slabs, written 1 KB per store instead of 64 scattered words
+// (config 5: 268 -> 134 MB written by K2 and read here)
+__global__ __launch_bounds__(256) void k_m3_reduce32(const float* __restrict__ part, double* M3,
+                                                     int64_t count, int nparts, int RP, const int* stop) {
     if (*stop) return;
     const int lane = threadIdx.x & 63, qd = threadIdx.x >> 6;
     const int64_t e = (int64_t)blockIdx.x * 64 + lane;
     double s = 0.0;
     if (e < count)
-        for (int y = qd; y < nparts; y += 4) s += part[(int64_t)y * count + e];
+        for (int y0 = qd; y0 < nparts; y0 += 64) {  // 16 loads in flight, then the in-order sum
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int y = y0 + 4 * u;
+                v[u] = y < nparts ? part[(int64_t)y * count + e] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (y0 + 4 * u < nparts) s += (double)v[u];
+        }
     __shared__ double red[4][64];
     red[qd][lane] = s;
     __syncthreads();
-    if (qd == 0 && e < count)
-        M3[e] = (double)(float)(((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+    if (qd == 0 && e < count) {
+        const int MT = RP >> 4;
+        const int rr = (int)(e & 3), l = (int)((e >> 2) & 63);
+        const int64_t mt = e >> 8;
+        const int64_t m = mt % MT, ttl = mt / MT;
+        const int64_t t = ttl * 16 + (l & 15), k = 16 * m + 4 * (l >> 4) + rr;
+        M3[t * RP + k] = (double)(float)(((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+    }
 }
 
 void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double* Bh, double* part,
@@ -366,8 +385,8 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
 #undef M3F_CASE
     TRITD_CHECK_LAUNCH();
     const int64_t count = g.n3p * g.RP;
-    hipLaunchKernelGGL(k_m3_reduce32, dim3((unsigned)cdiv(count, 64)), dim3(256), 0, st, part, M3,
-                       count, (int)(qper * jc), stop);
+    hipLaunchKernelGGL(k_m3_reduce32, dim3((unsigned)cdiv(count, 64)), dim3(256), 0, st,
+                       reinterpret_cast<const float*>(part), M3, count, (int)(qper * jc), g.RP, stop);
     TRITD_CHECK_LAUNCH();
 }
 
@@ -381,6 +400,7 @@ void launch_m3_32(const Geom& g, const float* T, const double* Ah, const double*
 // k_apply_gen).
 // ---------------------------------------------------------------------------
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 template <int RP, typename TM>
 __global__ __launch_bounds__(256) void k_apply_mfma(const TM* __restrict__ M, int64_t rows,
@@ -388,7 +408,7 @@ __global__ __launch_bounds__(256) void k_apply_mfma(const TM* __restrict__ M, in
                                                     double* YT, int64_t ldT, float* YF,
                                                     int round32, const int* stop) {
     if (stop && *stop) return;
-    constexpr int NT = RP / 16, KS = RP / 4, BATCH = KS < 16 ? KS : 16;
+    constexpr int NT = RP / 16, KS = RP / 4;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t tile = (int64_t)blockIdx.x * 4 + w;
     const int64_t rt = tile / NT;
@@ -397,30 +417,67 @@ __global__ __launch_bounds__(256) void k_apply_mfma(const TM* __restrict__ M, in
     if (r0 >= rows) return;  // wave-uniform
     const int m = lane & 15, kq = lane >> 4;
     const bool in = r0 + m < rows;
-    const TM* mp = M + (in ? (r0 + m) * RP : 0) + kq;
-    const double* gp = Ginv + (int64_t)kq * RP + 16 * ct + m;
+    // K-steps in groups of four consecutive k per lane: at K-step 4g + u lane
+    // (m, kq) takes k = 16 g + 4 kq + u, so one 16-byte (float) or two
+    // 16-byte (double) loads of M serve four K-steps (the word-per-step form
+    // took 34 us per apply at config 5).  Any k order is a valid MFMA sum;
+    // this one is fixed.
+    const TM* mp = M + (in ? (r0 + m) * RP : 0) + 4 * kq;
+    const double* gp = Ginv + (int64_t)(4 * kq) * RP + 16 * ct + m;
+    constexpr int NG = KS / 4, GB = NG < 4 ? NG : 4;
     d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int s0 = 0; s0 < KS; s0 += BATCH) {
-        double a[BATCH], b[BATCH];
+    for (int g0 = 0; g0 < NG; g0 += GB) {
+        double a[GB][4], b[GB][4];
 #pragma unroll
-        for (int u = 0; u < BATCH; ++u) {
-            a[u] = in ? (double)mp[4 * (s0 + u)] : 0.0;
-            b[u] = gp[(int64_t)4 * (s0 + u) * RP];
+        for (int gb = 0; gb < GB; ++gb) {
+            const int g = g0 + gb;
+            if constexpr (sizeof(TM) == 4) {
+                typedef float f4l __attribute__((ext_vector_type(4)));
+                const f4l v = in ? *reinterpret_cast<const f4l*>(mp + 16 * g) : f4l{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) a[gb][u] = (double)v[u];
+            } else {
+                const d2v v0 = in ? *reinterpret_cast<const d2v*>(mp + 16 * g) : d2v{0.0, 0.0};
+                const d2v v1 = in ? *reinterpret_cast<const d2v*>(mp + 16 * g + 2) : d2v{0.0, 0.0};
+                a[gb][0] = v0[0];
+                a[gb][1] = v0[1];
+                a[gb][2] = v1[0];
+                a[gb][3] = v1[1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) b[gb][u] = gp[(int64_t)(16 * g + u) * RP];
         }
 #pragma unroll
-        for (int u = 0; u < BATCH; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+        for (int gb = 0; gb < GB; ++gb)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[gb][u], b[gb][u], acc, 0, 0, 0);
     }
     const int k = 16 * ct + m;
+    // YT through a per-wave LDS tile: each lane then writes 16 consecutive i
+    // of one k-row (128-byte pieces) instead of one word per row
+    __shared__ double tl[4][16 * 17];
+    double* tw = tl[w];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int64_t i = r0 + kq + 4 * r;
-        if (i >= rows) continue;
         double v = acc[r];
         if (round32) v = (double)(float)v;
+        tw[(kq + 4 * r) * 17 + m] = v;
+        if (i >= rows) continue;
         Y[i * RP + k] = v;
-        if (YT) YT[(int64_t)k * ldT + i] = v;
         if (YF) YF[i * RP + k] = (float)v;
+    }
+    if (YT) {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const int64_t i = r0 + m;  // lane m: row i; kq + 4 r: the k-row
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int kk = kq + 4 * r;
+            if (i < rows) YT[(int64_t)(16 * ct + kk) * ldT + i] = tw[m * 17 + kk];
+        }
     }
 }
 

@@ -179,7 +179,107 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
     }
 }
 
+// The same with TWO ij-tiles per wave (32 consecutive i of one fibre j,
+// mode 0, RP <= 64): both accumulate against the same C^T operand read, and
+// before the stores v_permlane16_swap pairs their rows so that one store
+// instruction writes two t-rows of 32 i = 2 x 256 B (the one-tile form stores
+// 4 x 128 B pieces, one per t-row).  Needs qper even (both tiles in one j).
+template <int RP>
+__global__ __launch_bounds__(64 * TP_WAVES) void k_tp2(const double* __restrict__ Ah,
+                                                       const double* __restrict__ Bh,
+                                                       const double* __restrict__ ChT, double* L,
+                                                       int64_t n1p, int64_t n1l, int64_t n3,
+                                                       int64_t n3p, int64_t tiles, int64_t ldj,
+                                                       int64_t ldt, int64_t ahj, int64_t bhj) {
+    constexpr int KS = RP / 4;
+    constexpr int SK = 17;
+    constexpr int NT = 64 * TP_WAVES;
+    constexpr int SP = RP * 8;
+    constexpr int NS = (SP + NT - 1) / NT;
+    __shared__ double sct[2][RP * SK];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int il = lane & 15, tg = lane >> 4;
+    const int64_t tile0 = ((int64_t)blockIdx.x * TP_WAVES + wid) * 2;  // tiles tile0, tile0 + 1
+    const bool active = tile0 < tiles;
+    const int64_t qper = n1p >> 4;
+    const int64_t j = active ? tile0 / qper : 0;
+    const int64_t i0 = active ? (tile0 - j * qper) << 4 : 0;  // first i of the 32
+    double kr0[KS], kr1[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int k = 4 * s + tg;
+        const double b = active ? Bh[j * bhj + k] : 0.0;
+        kr0[s] = active ? Ah[j * ahj + (i0 + il) * RP + k] * b : 0.0;
+        kr1[s] = active ? Ah[j * ahj + (i0 + 16 + il) * RP + k] * b : 0.0;
+    }
+    const int64_t ntt = n3p >> 4;
+    d2v sv[NS];
+    auto stage_load = [&](int64_t tt) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * NT;
+            if (SP % NT == 0 || e < SP) {
+                const int k = e >> 3, t = (e & 7) * 2;
+                sv[q] = *reinterpret_cast<const d2v*>(ChT + (int64_t)k * n3p + tt * 16 + t);
+            }
+        }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int e = threadIdx.x + q * NT;
+            if (SP % NT == 0 || e < SP) {
+                const int k = e >> 3, t = (e & 7) * 2;
+                sct[buf][k * SK + t] = sv[q][0];
+                sct[buf][k * SK + t + 1] = sv[q][1];
+            }
+        }
+    };
+    // after the swap lane l holds i = i0 + (l & 31) at t-row 2 (l >> 5) (+1 in
+    // the second register) of each group of four
+    const int64_t irow = i0 + (lane & 31);
+    const bool row_ok = active && irow < n1l;
+    const int64_t obase = irow + ldj * j;
+    const int th = 2 * (lane >> 5);
+    auto swap = [](double x, double y, double& a, double& b) {
+        const unsigned xl = __double2loint(x), xh = __double2hiint(x);
+        const unsigned yl = __double2loint(y), yh = __double2hiint(y);
+        const auto lo = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+        a = __hiloint2double((int)hi[0], (int)lo[0]);
+        b = __hiloint2double((int)hi[1], (int)lo[1]);
+    };
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    for (int64_t tt = 0; tt < ntt; ++tt) {
+        const int buf = (int)(tt & 1);
+        const bool more = tt + 1 < ntt;
+        if (more) stage_load(tt + 1);
+        const double* cT = sct[buf];
+        d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const double c = cT[(4 * s + tg) * SK + il];
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(c, kr0[s], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(c, kr1[s], acc1, 0, 0, 0);
+        }
+        // C/D element r of lane l: t = 16 tt + (l>>4) + 4r, i = i0 (+16 in acc1) + (l&15)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            double a, b;
+            swap(acc0[rr], acc1[rr], a, b);
+            const int64_t t = tt * 16 + 4 * rr + th;
+            if (row_ok && t < n3) __builtin_nontemporal_store(a, L + obase + ldt * t);
+            if (row_ok && t + 1 < n3) __builtin_nontemporal_store(b, L + obase + ldt * (t + 1));
+        }
+        if (more) stage_store(buf ^ 1);
+        __syncthreads();
+    }
+}
+
 int tp_grid(const Geom& g) { return (int)cdiv(g.tiles, TP_WAVES); }
+static bool tp2_ok(const Geom& g) { return g.RP <= 64 && ((g.n1p >> 4) & 1) == 0; }
 
 void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* ChT, double* Lout,
                const double* X, double* partial, int mode, int64_t ldj, int64_t ldt,
@@ -187,6 +287,26 @@ void launch_tp(const Geom& g, const double* Ah, const double* Bh, const double* 
     if (bhj < 0) bhj = g.RP;
     if (g.n3p % 16) throw Error(TRITD_ERR_ARG, "triple_product: n3p must be a multiple of 16");
     const dim3 grid(tp_grid(g)), block(64 * TP_WAVES);
+#ifndef TP_TWO
+#define TP_TWO 1
+#endif
+    if (TP_TWO && mode == 0 && tp2_ok(g)) {
+        const dim3 grid2((unsigned)cdiv(g.tiles, 2 * TP_WAVES));
+#define TP2_CASE(RPV)                                                                                \
+    case RPV:                                                                                        \
+        hipLaunchKernelGGL((k_tp2<RPV>), grid2, block, 0, st, Ah, Bh, ChT, Lout, g.n1p, g.n1l, g.n3,   \
+                           g.n3p, g.tiles, ldj, ldt, ahj, bhj);                                      \
+        break;
+        switch (g.RP) {
+            TP2_CASE(16)
+            TP2_CASE(32)
+            TP2_CASE(48)
+            TP2_CASE(64)
+        }
+#undef TP2_CASE
+        TRITD_CHECK_LAUNCH();
+        return;
+    }
 #define TP_CASE(RPV)                                                                                 \
     case RPV:                                                                                        \
         if (mode == 0)                                                                               \
