@@ -69,3 +69,21 @@ def test_f32_r16_repeat_bitwise(tritd):
     D = d["D"].astype(np.float32)
     first = _solve(tritd, D, 16, opts, d, {})
     _same(_solve(tritd, D, 16, opts, d, {}), first)
+
+
+@pytest.mark.parametrize("n1", [96, 80])  # 6 i-tiles: the two-tile form (k_tp2); 5: the one-tile form
+def test_triple_product_repeat_bitwise(tritd, n1):
+    """`triple_product` (k_tp2 pairs accumulator rows across lanes before its
+    stores) twice on the same factors: bitwise equal, and within rounding of
+    the oracle's product (triple_product.m:6)."""
+    rng = np.random.default_rng(7)
+    r = 8
+    A = rng.standard_normal((n1, r, r))
+    B = rng.standard_normal((r, 72, r))
+    C = rng.standard_normal((r, r, 40))
+    L1 = tritd.triple_product(A, B, C)
+    L2 = tritd.triple_product(A, B, C)
+    assert np.array_equal(L1, L2), "repeat differs"
+    import tritd_oracle as orc
+    ref = orc.triple_product(A, B, C)
+    assert np.max(np.abs(L1 - ref)) <= 1e-12 * np.max(np.abs(ref))
