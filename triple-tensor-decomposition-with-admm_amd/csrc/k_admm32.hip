@@ -448,7 +448,8 @@ void k5_f32s(K5Args32 a) {
     // W granules (of 4 M-tiles) of the h = 0 wave, which also runs the
     // elementwise chain; h = 1 holds the other G - GH0 (round 5: 1 of 4 vs
     // 2 of 4: K5 13.65 vs 13.75 ms; the L K-steps split 4:12 or 12:4 instead
-    // of 8:8: 14.00 / 14.02 ms — profiles/round5/ab_k5_split.txt)
+    // of 8:8: 14.00 / 14.02 ms — profiles/round5/ab_k5_split.txt; with the
+    // roles alternated per round below, 1 : 3 is 13.39 ms and 2 : 2 13.82)
     constexpr int GH0 = 1;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -720,13 +721,19 @@ void k5_f32s(K5Args32 a) {
                 wl[slot * WS + k * 16 + il] = wacc[mq][rr];
             }
     };
-    // the pair's roles alternate between workgroups (the h = 0 wave carries
-    // the elementwise chain; the two workgroups resident on a CU then put it
-    // on different SIMDs, as far as waves map to SIMDs in order)
     // (Walking pairs grid-stride in 512 persistent workgroups instead, to
     // save the turnover of 131 072 short-lived ones: K5 15.88 vs 13.79 ms,
     // profiles/round5/ab_c5_prologue_persistent.txt — dropped.)
-    const int hrole = (wid & 1) ^ (int)(blockIdx.x & 1);
+    // Roles alternate between workgroups that share a CU, so that each SIMD
+    // hosts one chain wave (h = 0) and one partner: blocks are dealt to the
+    // XCDs by blockIdx mod 8, so the two resident on a CU have the same
+    // blockIdx parity but sit one round of `slots` apart (and a retiring
+    // workgroup is replaced by one a whole number of rounds later).  Round
+    // 5: alternating by blockIdx parity put both chain waves of a CU on the
+    // same two SIMDs (K5 13.57 vs 13.39 ms with the 1 : 3 W split; with 2 : 2
+    // 13.68 vs 13.82 — profiles/round5/ab_k5_roles.txt)
+    const int64_t rnd = a.slots > 0 ? (int64_t)blockIdx.x / a.slots : (int64_t)blockIdx.x;
+    const int hrole = (wid & 1) ^ (int)(rnd & 1);
     if (hrole)
         walk(std::integral_constant<int, 1>{});
     else
@@ -771,7 +778,14 @@ int k5_parts32(const Geom& g) { return k5_split32(g) ? (int)cdiv(g.tiles, 2) : k
 
 void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st) {
     if (!prologue && k5_split32(g)) {
-        hipLaunchKernelGGL(k5_f32s<256>, dim3((unsigned)k5_parts32(g)), dim3(256), 0, st, a);
+        static int cus[64] = {0};
+        int dev = 0;
+        TRITD_HIP(hipGetDevice(&dev));
+        int& n = cus[dev & 63];
+        if (!n) TRITD_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        K5Args32 b = a;
+        b.slots = (int64_t)n;  // one workgroup per CU per round of dispatch
+        hipLaunchKernelGGL(k5_f32s<256>, dim3((unsigned)k5_parts32(g)), dim3(256), 0, st, b);
         TRITD_CHECK_LAUNCH();
         return;
     }

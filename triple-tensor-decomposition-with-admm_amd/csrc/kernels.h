@@ -273,6 +273,7 @@ struct K5Args32 {
     IterScalars32 s;
     const int* stop;
     unsigned long long* dense_tiles;
+    int64_t slots;  // workgroups resident at once (2 per CU): the pair roles alternate per round
 };
 constexpr int CE32_SLOT = 64;  // floats per compact-E slot (50 values, their position bytes, the count)
 bool rp_supported32(int RP);
