@@ -7,7 +7,7 @@ make -j8 >/dev/null
 mkdir -p ../../ab
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  rm -rf build_$name; cp -r build build_$name; rm -f build_$name/k_*.o
+  rm -rf build_$name; cp -r build build_$name; rm -f build_$name/k_*.o build_$name/solver.o build_$name/api.o
   make OBJDIR=build_$name OUT=../../ab/$name.so EXTRA="$flags" >/dev/null &
 done
 wait
