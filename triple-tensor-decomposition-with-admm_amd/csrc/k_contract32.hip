@@ -132,19 +132,21 @@ __global__ __launch_bounds__(256) void k_m2_32v(const float* __restrict__ Wk,
 // the row k of A^T (n1p doubles, rounded to single once) is loaded once per
 // JB rows instead of once per row (k_m2_32v re-read all of A^T for every j:
 // 8.6 GB of L2 traffic beside the 4.3 GB of W at config 5).  n1p <= 64*4*UG.
-// The extra column of workgroups (fin.on): the previous iteration's norm
-// reduction and stop test in its first one, as k_m1 (k_contract.hip) — here
-// rather than in M1, whose 2 048 workgroups are one full round of the chip
-// (an extra one there lengthened M1 by ~60 us, config 5).  M1, apply A and
-// Gram A before it write only scratch and this iteration's A^ parity buffer.
+// fin.on: workgroup (0, 0) first runs the previous iteration's norm
+// reduction and stop test (finish.h), then its own rows — here rather than
+// in M1, whose 2 048 workgroups are one full round of the chip (an extra one
+// there lengthened M1 by ~60 us, config 5), and inside a workgroup of M2's
+// 13 rounds rather than an extra column of them (which lengthened M2 by
+// ~40 us).  M1, apply A and Gram A before it write only scratch and this
+// iteration's A^ parity buffer.
 template <int UG, int JB>
 __global__ __launch_bounds__(256) void k_m2_32w(const float* __restrict__ Wk,
                                                 const double* __restrict__ AhT, double* M2,
                                                 int64_t n1p, int64_t n2, int64_t plane, int RP,
                                                 const int* stop, FinishArgs fin) {
-    if (fin.on && blockIdx.x == gridDim.x - 1) {
-        if (blockIdx.y == 0) reduce_finish_wg<256>(fin);
-        return;
+    if (fin.on && blockIdx.x == 0 && blockIdx.y == 0) {
+        reduce_finish_wg<256>(fin);
+        __syncthreads();
     }
     if (*stop) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -195,7 +197,7 @@ void launch_m2_32(const Geom& g, const float* Wk, const double* AhT, double* M2,
                   hipStream_t st, const FinishArgs& fin) {
     constexpr int UG = 8, JB = 8;
     if (g.n1p <= 64 * 4 * UG) {
-        hipLaunchKernelGGL((k_m2_32w<UG, JB>), dim3((unsigned)cdiv(g.n2, 4 * JB) + (fin.on ? 1 : 0), (unsigned)g.RP),
+        hipLaunchKernelGGL((k_m2_32w<UG, JB>), dim3((unsigned)cdiv(g.n2, 4 * JB), (unsigned)g.RP),
                            dim3(256), 0, st, Wk, AhT, M2, g.n1p, g.n2, g.plane, g.RP, stop, fin);
         TRITD_CHECK_LAUNCH();
         return;
