@@ -17,6 +17,7 @@
 // l: words 0..49 the nonzeros in (w, lane) order, bytes 200..249 their tile
 // positions 4 lane + w, word 63 the count; more than 50 nonzeros -> the tile
 // is stored densely in E and its count is all ones (ce32_decode below).
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -778,11 +779,16 @@ int k5_parts32(const Geom& g) { return k5_split32(g) ? (int)cdiv(g.tiles, 2) : k
 
 void launch_k5_32(const Geom& g, const K5Args32& a, bool prologue, hipStream_t st) {
     if (!prologue && k5_split32(g)) {
-        static int cus[64] = {0};
+        // CU count per device, cached (shard threads of a device set may race
+        // to fill an entry: both store the same value)
+        static std::atomic<int> cus[64];
         int dev = 0;
         TRITD_HIP(hipGetDevice(&dev));
-        int& n = cus[dev & 63];
-        if (!n) TRITD_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        int n = cus[dev & 63].load(std::memory_order_relaxed);
+        if (!n) {
+            TRITD_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+            cus[dev & 63].store(n, std::memory_order_relaxed);
+        }
         K5Args32 b = a;
         b.slots = (int64_t)n;  // one workgroup per CU per round of dispatch
         hipLaunchKernelGGL(k5_f32s<256>, dim3((unsigned)k5_parts32(g)), dim3(256), 0, st, b);
