@@ -527,6 +527,12 @@ static M3Cp m3_cp_split(const Geom& g) {
 // the CP model's K2 (k_m3_cp); Qi's H rows change with j (k_m3)
 static bool m3_use_cp(int64_t ahj) { return ahj == 0; }
 
+static int current_device() {
+    int d = 0;
+    TRITD_HIP(hipGetDevice(&d));
+    return d;
+}
+
 int m3_parts(const Geom& g) {
     const int a = m3_split(g) / 4, b = m3_cp_split(g).S / 4;
     return a > b ? a : b;
@@ -548,19 +554,16 @@ void launch_m3(const Geom& g, const double* T, const double* Ah, const double* B
 #define M3_CASE(RPV, LDAV, KOFF)                                                              \
     {                                                                                         \
         const size_t lds = (size_t)2 * (RPV / 16) * 16 * 64 * sizeof(double);                \
-        static bool attr_set = false;                                                         \
-        if (!attr_set) {                                                                      \
+        static std::atomic<uint64_t> attr_set{0}; /* per device (bit), device-set threads */  \
+        const uint64_t dbit = (uint64_t)1 << (current_device() & 63);                          \
+        if (!(attr_set.load(std::memory_order_acquire) & dbit)) {                               \
             TRITD_HIP(hipFuncSetAttribute((const void*)k_m3<RPV, LDAV>,                       \
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-            attr_set = true;                                                                  \
+            TRITD_HIP(hipFuncSetAttribute((const void*)k_m3_cp<RPV, LDAV>,                    \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+            attr_set.fetch_or(dbit, std::memory_order_acq_rel);                                \
         }                                                                                     \
         if (cp) {                                                                             \
-            static bool attr_cp = false;                                                      \
-            if (!attr_cp) {                                                                   \
-                TRITD_HIP(hipFuncSetAttribute((const void*)k_m3_cp<RPV, LDAV>,                \
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-                attr_cp = true;                                                               \
-            }                                                                                 \
             hipLaunchKernelGGL((k_m3_cp<RPV, LDAV>), dim3(grid.x + side.on), dim3(256), lds, st, T, \
                                Ah + (KOFF), Bh + (KOFF), part + (KOFF), g.n2, g.n3p, g.ntt, cs.qper, \
                                cs.J, S, stop, side);                                 \
