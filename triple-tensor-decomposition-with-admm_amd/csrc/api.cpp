@@ -185,8 +185,13 @@ public:
             ++s_->busy;
         }
         lk_ = std::unique_lock<std::mutex>(s_->m);
+        // (on the null stream the last call's kernels precede this one's in
+        // stream order already, and its handle is never reused: no wait.  Round
+        // 5 saw one run in ~10 where the null-stream wait left the thread's
+        // last error set to "event last recorded in a capturing stream" while
+        // returning success, failing the next launch check.)
         if (!s_->done) TRITD_HIP(hipEventCreateWithFlags(&s_->done, hipEventDisableTiming));
-        else TRITD_HIP(hipStreamWaitEvent(st, s_->done, 0));
+        else if (st != nullptr) TRITD_HIP(hipStreamWaitEvent(st, s_->done, 0));
     }
     ~ScratchLease() {
         lk_.unlock();
