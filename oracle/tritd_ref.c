@@ -505,3 +505,76 @@ int tritd_ref_admm_f32(const float* D, idx n1, idx n2, idx n3, int r, const doub
 
 int tritd_ref_threads(void) { return omp_get_max_threads(); }
 void tritd_ref_set_threads(int n) { omp_set_num_threads(n); }
+
+
+/* ------------------------------------------- lean single-precision form */
+/* Building blocks of oracle/tritd_lean.py: the same class-single solver as
+ * tritd_ref_admm_f32 (every elementwise statement of :33,:41-53 evaluated in
+ * single with the same single scalars, L double and rounded to single where
+ * it meets D), organised so that a 2048x2048x256 r=16 problem fits a 64 GB
+ * host: T, O, E, Y_L, Y_O stay single, the permute copies and design matrices
+ * are never materialised (the MTTKRPs are BLAS GEMMs on row blocks, driven
+ * from Python), and L is formed one frontal slice (fixed t) at a time.
+ * TEST INFRASTRUCTURE ONLY. */
+
+/* T = D - O + (1/muL)*Y_L in single (:33) */
+void tritd_ref_lean_form_T(const float* D, const float* O, const float* YL, double muL, float* T,
+                           idx N) {
+    const float invL = (float)(1.0 / muL);
+#pragma omp parallel for schedule(static)
+    for (idx e = 0; e < N; ++e) T[e] = (D[e] - O[e]) + invL * YL[e];
+}
+
+/* sum of squares of a single array, in double (norm(D(:)) at :28) */
+double tritd_ref_lean_sumsq(const float* X, idx N) {
+    double s = 0;
+#pragma omp parallel for reduction(+ : s) schedule(static)
+    for (idx e = 0; e < N; ++e) s += (double)X[e] * (double)X[e];
+    return s;
+}
+
+/* :41-53 on one slice of n elements, given L of that slice in double; the
+ * slice's sums of resL^2 and resO^2 go to sums[0], sums[1] (statement for
+ * statement the loop body of tritd_ref_admm_f32) */
+void tritd_ref_lean_update(const float* D, float* O, float* E, float* YL, float* YO,
+                           const double* L, idx n, double muL, double muO, double lambda,
+                           double* sums) {
+    const float invL = (float)(1.0 / muL), invO = (float)(1.0 / muO);
+    const float fmuL = (float)muL, fmuO = (float)muO;
+    const float den = (float)(muL + muO), thr = (float)(lambda / muO);
+    double sL = 0, sO = 0;
+#pragma omp parallel for reduction(+ : sL, sO) schedule(static)
+    for (idx e = 0; e < n; ++e) {
+        const float d = D[e], Lf = (float)L[e], yl = YL[e], yo = YO[e];
+        const float R1 = (d - Lf) + invL * yl;                             /* :41 */
+        const float R2 = E[e] - invO * yo;                                 /* :42 */
+        const float On = (fmuL * R1 + fmuO * R2) / den;                    /* :43 */
+        const float R3 = On + invO * yo;                                   /* :46 */
+        const float sg = R3 > 0 ? 1.0f : (R3 < 0 ? -1.0f : (R3 == 0 ? 0.0f : R3));
+        const float En = sg * fmaxf(fabsf(R3) - thr, 0.0f);                /* :47 */
+        const float rL = (d - Lf) - On;                                    /* :50 */
+        const float rO = On - En;                                          /* :51 */
+        YL[e] = yl + fmuL * rL;                                            /* :52 */
+        YO[e] = yo + fmuO * rO;                                            /* :53 */
+        O[e] = On;
+        E[e] = En;
+        sL += (double)rL * (double)rL;
+        sO += (double)rO * (double)rO;
+    }
+    sums[0] = sL;
+    sums[1] = sO;
+}
+
+/* sum over a slice of (L - X)^2 and X^2 in double, X single (the driver's
+ * evaluate, traffic_triple_comparison.m:194-199) */
+void tritd_ref_lean_rre_parts(const double* L, const float* X, idx n, double* parts) {
+    double a = 0, b = 0;
+#pragma omp parallel for reduction(+ : a, b) schedule(static)
+    for (idx e = 0; e < n; ++e) {
+        const double x = X[e], d = L[e] - x;
+        a += d * d;
+        b += x * x;
+    }
+    parts[0] = a;
+    parts[1] = b;
+}

@@ -71,7 +71,10 @@ def test_f32_r16_repeat_bitwise(tritd):
     _same(_solve(tritd, D, 16, opts, d, {}), first)
 
 
-@pytest.mark.parametrize("n1", [96, 80])  # 6 i-tiles: the two-tile form (k_tp2); 5: the one-tile form
+# 96: 6 i-tiles, the two-tile form (k_tp2); 90: the same form with 6 padded
+# rows in its last i-tile (row mask, paired stores of a partial tile; ADVICE
+# r5); 80: 5 i-tiles, the one-tile form
+@pytest.mark.parametrize("n1", [96, 90, 80])
 def test_triple_product_repeat_bitwise(tritd, n1):
     """`triple_product` (k_tp2 pairs accumulator rows across lanes before its
     stores) twice on the same factors: bitwise equal, and within rounding of

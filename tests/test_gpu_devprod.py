@@ -161,3 +161,53 @@ def test_dev_products_on_more_streams_than_the_scratch_cap(env):
         assert rel(_host(X, s), refs[c]) <= 1e-13
     for st in streams:
         st.close()
+
+
+def test_products_after_destroyed_streams_leave_no_error(env):
+    """Round 5's intermittent failure (profiles/round5/gpu_tests_null_stream_
+    wait_failure.log.txt), its condition made deliberate: scratch entries whose
+    `done` events were last recorded on streams that have since been destroyed
+    fill the cache; then host-form products on the null stream (new entry:
+    eviction; growing sizes: scratch regrow), device-form products on new
+    streams (more evictions) and a tritd_shutdown.  On ROCm 7.2 a host wait on
+    such an event (hipEventSynchronize) reads the freed stream object and, when
+    that memory happens to read "capture active", returns
+    hipErrorCapturedEvent — which an unchecked call left behind for the next
+    launch check.  The library now never waits on those events from the host
+    (api.cpp ScratchSet); every call must succeed and leave the thread's HIP
+    error state clear."""
+    import tritd_oracle as orc
+    from tritd import synth
+    hip, tritd, check, lib = env
+    rt = hip.rt
+    rt.hipPeekAtLastError.restype = C.c_int
+    s = (40, 32, 30, 8)
+    h, t = _case(hip, *s, seed=300)
+    hip.synchronize()
+    for rep in range(3):
+        streams = [hip.Stream() for _ in range(20)]
+        for st in streams:
+            X = hip.DeviceArray(s[0] * s[1] * s[2] * 8)
+            _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X, st.handle)
+            X.free()
+        for st in streams:  # destroyed with their entries still cached
+            st.close()
+        # churn the host heap where the stream objects were
+        junk = [hip.Stream() for _ in range(8)]
+        for st in junk:
+            st.close()
+        for q, n in enumerate((24, 48, 72)):  # null stream: new entry, then regrowth
+            A, B, Cc = synth.random_factors(n, n - 4, n - 8, 8, seed=310 + q)
+            L = tritd.triple_product(A, B, Cc)
+            assert rt.hipPeekAtLastError() == 0
+            assert rel(L, orc.triple_product(A, B, Cc)) <= 1e-13
+        st2 = hip.Stream()
+        X = hip.DeviceArray(s[0] * s[1] * s[2] * 8)
+        _launch(lib, check, lib.tritd_dev_triple_product_f64, t, s, X, st2.handle)
+        st2.synchronize()
+        assert rel(_host(X, s), tritd.triple_product(*h)) <= 1e-13
+        X.free()
+        st2.close()
+        assert rt.hipPeekAtLastError() == 0
+        lib.tritd_shutdown()
+        assert rt.hipPeekAtLastError() == 0

@@ -255,7 +255,10 @@ def test_soft_threshold_bit_exact(tritd, orc):
         np.testing.assert_array_equal(tritd.soft_threshold(Y, 0.7), orc.soft_threshold(Y, 0.7))
 
 
-@pytest.mark.parametrize("n1,n2,n3,r", [(12, 10, 8, 2), (30, 31, 29, 3), (17, 16, 20, 8), (5, 4, 33, 5)])
+# r = 12 and 16 (R = 144 / 256, the padded-rank 256 kernel config 5's
+# reconstruction runs, traffic_triple_comparison.m:62) beside the r <= 8 forms
+@pytest.mark.parametrize("n1,n2,n3,r", [(12, 10, 8, 2), (30, 31, 29, 3), (17, 16, 20, 8), (5, 4, 33, 5),
+                                        (40, 36, 30, 12), (33, 20, 48, 16), (64, 64, 32, 16)])
 def test_triple_product(tritd, orc, n1, n2, n3, r):
     from tritd import synth
     A, B, C = synth.random_factors(n1, n2, n3, r, seed=n1)

@@ -112,11 +112,11 @@ AlsSession::AlsSession(int device, const double* X, int64_t ldX, int64_t n1, int
 }
 
 AlsSession::~AlsSession() {
-    (void)hipSetDevice(device_);
-    if (st_) (void)hipStreamSynchronize(st_);
-    for (auto e : ev_) (void)hipEventDestroy(e);
-    if (ctrl_) (void)hipFree(ctrl_);
-    if (own_stream_ && st_) (void)hipStreamDestroy(st_);
+    hip_quiet(hipSetDevice(device_));
+    if (st_) hip_quiet(hipStreamSynchronize(st_));
+    for (auto e : ev_) hip_quiet(hipEventDestroy(e));
+    if (ctrl_) hip_quiet(hipFree(ctrl_));
+    if (own_stream_ && st_) hip_quiet(hipStreamDestroy(st_));
 }
 
 void AlsSession::set_norm_from_red0() {
@@ -273,7 +273,7 @@ void AlsSession::harvest_timing() {
         acc_m3_ += m3;
         ++acc_n_;
     }
-    for (auto e : ev_) (void)hipEventDestroy(e);
+    for (auto e : ev_) hip_quiet(hipEventDestroy(e));
     ev_.clear();
 }
 

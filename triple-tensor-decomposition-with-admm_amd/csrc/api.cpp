@@ -143,14 +143,33 @@ std::vector<ncclComm_t> g_comms;
 // frees it.  (Stream-ordered hipMallocAsync scratch on the null stream read
 // back as zeros on a repeated call on ROCm 7.2: tools/rounds/r4/iso_tp.sh, round 4.)
 // The entry's `done` event marks the end of the last call's kernels: a call
-// waits on it (device side) before overwriting the buffers, which orders it
-// after that call even when a destroyed stream's handle is reused.
+// makes its stream wait on it (device side) before overwriting the buffers,
+// which orders it after that call even when a destroyed stream's handle is
+// reused.
+//
+// The host never waits on `done` (hipEventSynchronize / hipEventQuery): the
+// stream it was last recorded on may be one the caller has destroyed since,
+// and on ROCm 7.2 both calls read the event's stream object without checking
+// that it is alive — if the freed memory holds "capture active" in the
+// stream's capture-status word, they write "invalidated" into it and return
+// hipErrorCapturedEvent ("operation not permitted on an event last recorded
+// in a capturing stream"; libamdhip64 7.2.70200, hipEventSynchronize at
+// 0x9a552..0x9ac90, hipEventQuery at 0x99b2c..0x99cd0).  That is round 5's
+// intermittent failure (profiles/round5/gpu_tests_null_stream_wait_failure.
+// log.txt): test_gpu_devprod.py left 16 entries of 24 destroyed streams; the
+// next null-stream product evicted one with an unchecked
+// hipEventSynchronize(victim->done), whose error stayed in the thread's last
+// error and failed the following launch check.  hipStreamWaitEvent checks the
+// recording stream's handle before using it, so the device-side wait is
+// safe.  Host-side waits are now hipStreamSynchronize on the caller's (live)
+// stream after that wait, or hipDeviceSynchronize where no stream of the
+// entry is known (eviction, tritd_shutdown).  DESIGN.md §6.
 // Bounded: at most SCRATCH_CAP entries; a new (device, stream)
-// beyond that evicts the least recently used entry after its last product
-// has finished (its event).  Each entry has its own lock, held over one
-// call's enqueue (two host threads on one stream would otherwise interleave
-// their packs and products); the map's lock is held only to find, insert or
-// evict an entry, so calls on different streams do not serialise.
+// beyond that evicts the least recently used entry after the device has
+// drained.  Each entry has its own lock, held over one call's enqueue (two
+// host threads on one stream would otherwise interleave their packs and
+// products); the map's lock is held only to find, insert or evict an entry,
+// so calls on different streams do not serialise.
 struct ScratchSet {
     std::array<DBuf, 5> buf;
     hipEvent_t done = nullptr;
@@ -158,7 +177,9 @@ struct ScratchSet {
     uint64_t used = 0;  // LRU stamp (under g_scratch_mutex)
     int busy = 0;       // calls holding or waiting for m (under g_scratch_mutex)
     ~ScratchSet() {
-        if (done) (void)hipEventDestroy(done);
+        // (a destructor cannot report; a failure must not stay behind as the
+        // thread's last error either, or the next launch check would report it)
+        if (done && hipEventDestroy(done) != hipSuccess) (void)hipGetLastError();
     }
 };
 constexpr size_t SCRATCH_CAP = 16;
@@ -169,7 +190,7 @@ uint64_t g_scratch_clock = 0;
 // One call's hold on the (device, stream) entry: its lock for the enqueue.
 class ScratchLease {
 public:
-    explicit ScratchLease(hipStream_t st) {
+    explicit ScratchLease(hipStream_t st) : st_(st) {
         int dev = 0;
         TRITD_HIP(hipGetDevice(&dev));
         {
@@ -184,24 +205,32 @@ public:
             s_->used = ++g_scratch_clock;
             ++s_->busy;
         }
-        lk_ = std::unique_lock<std::mutex>(s_->m);
-        // (on the null stream the last call's kernels precede this one's in
-        // stream order already, and its handle is never reused: no wait.  Round
-        // 5 saw one run in ~10 where the null-stream wait left the thread's
-        // last error set to "event last recorded in a capturing stream" while
-        // returning success, failing the next launch check.)
-        if (!s_->done) TRITD_HIP(hipEventCreateWithFlags(&s_->done, hipEventDisableTiming));
-        else if (st != nullptr) TRITD_HIP(hipStreamWaitEvent(st, s_->done, 0));
+        // from here on the destructor owns the busy count: a HIP call below
+        // that throws must not leave the entry busy for good
+        try {
+            lk_ = std::unique_lock<std::mutex>(s_->m);
+            if (!s_->done) TRITD_HIP(hipEventCreateWithFlags(&s_->done, hipEventDisableTiming));
+            else TRITD_HIP(hipStreamWaitEvent(st, s_->done, 0));
+        } catch (...) {
+            release();
+            throw;
+        }
     }
-    ~ScratchLease() {
-        lk_.unlock();
-        std::lock_guard<std::mutex> lk(g_scratch_mutex);
-        --s_->busy;
-    }
+    ~ScratchLease() { release(); }
     ScratchSet& set() { return *s_; }
+    hipStream_t stream() const { return st_; }
 
 private:
-    // the least recently used idle entry leaves once the map is full
+    void release() {
+        if (!s_) return;
+        if (lk_.owns_lock()) lk_.unlock();
+        std::lock_guard<std::mutex> lk(g_scratch_mutex);
+        --s_->busy;
+        s_ = nullptr;
+    }
+    // the least recently used idle entry leaves once the map is full; its
+    // last product may still read the buffers (and its stream may be gone):
+    // drain the device, then free
     static void evict_locked() {
         if (g_scratch->size() < SCRATCH_CAP) return;
         auto victim = g_scratch->end();
@@ -210,19 +239,25 @@ private:
                 (victim == g_scratch->end() || it->second->used < victim->second->used))
                 victim = it;
         if (victim == g_scratch->end()) return;  // all in use: grow past the cap
-        if (victim->second->done) (void)hipEventSynchronize(victim->second->done);
+        TRITD_HIP(hipDeviceSynchronize());
         g_scratch->erase(victim);
     }
+    hipStream_t st_ = nullptr;
     ScratchSet* s_ = nullptr;
     std::unique_lock<std::mutex> lk_;
 };
 
-double* scratch(ScratchSet& s, int slot, size_t count) {
-    DBuf& b = s.buf[slot];
+// buffer `slot` of the lease's entry, grown on demand: the stream already
+// waits for the entry's last call (the lease), so once the stream has drained
+// no kernel reads the old buffer
+double* scratch(ScratchLease& lease, int slot, size_t count) {
+    DBuf& b = lease.set().buf[slot];
     if (b.p && b.n < count) {
-        TRITD_HIP(hipEventSynchronize(s.done));  // the last call may still read it
-        TRITD_HIP(hipFree(b.p));
+        TRITD_HIP(hipStreamSynchronize(lease.stream()));
+        double* old = b.p;
         b.p = nullptr;
+        b.n = 0;
+        TRITD_HIP(hipFree(old));
     }
     if (!b.p) b.alloc(count);
     return b.p;
@@ -230,14 +265,15 @@ double* scratch(ScratchSet& s, int slot, size_t count) {
 
 void drop_scratch() {
     std::lock_guard<std::mutex> lk(g_scratch_mutex);
-    if (!g_scratch) return;
+    if (!g_scratch || g_scratch->empty()) return;
+    // the last product on each stream may still read the buffers, and the
+    // streams may be gone: drain the device once
+    if (hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError();
     for (auto it = g_scratch->begin(); it != g_scratch->end();) {
         if (it->second && it->second->busy) {  // a call on another thread holds it
             ++it;
             continue;
         }
-        // the last product on the stream may still read the buffers
-        if (it->second && it->second->done) (void)hipEventSynchronize(it->second->done);
         it = g_scratch->erase(it);
     }
 }
@@ -279,19 +315,28 @@ void group_comms(const std::vector<int>& devs) {
     std::vector<ncclComm_t> cs((size_t)P, nullptr);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
+    // nothing inside the group throws: a failure is recorded, the
+    // group is always closed, and the communicators it started are aborted
+    hipError_t he = hipSuccess;
     r = ncclGroupStart();
     for (int p = 0; p < P && (r == ncclSuccess || r == ncclInProgress); ++p) {
-        TRITD_HIP(hipSetDevice(devs[p]));
+        he = hipSetDevice(devs[p]);
+        if (he != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
         r = ncclCommInitRankConfig(&cs[p], P, id, p, &cfg);
     }
     const ncclResult_t re = ncclGroupEnd();
     if (r == ncclInProgress) r = ncclSuccess;
     if (r == ncclSuccess && re != ncclInProgress) r = re;
-    for (int p = 0; p < P && r == ncclSuccess; ++p)
+    for (int p = 0; p < P && r == ncclSuccess && he == hipSuccess; ++p)
         if (cs[p]) r = nccl_settle(cs[p]);
-    if (r != ncclSuccess) {
+    if (r != ncclSuccess || he != hipSuccess) {
         for (ncclComm_t c : cs)
             if (c) (void)ncclCommAbort(c);
+        if (he != hipSuccess)
+            throw Error(TRITD_ERR_HIP, std::string("hipSetDevice (device group): ") + hipGetErrorString(he));
         throw Error(TRITD_ERR_RCCL, std::string("ncclCommInitRankConfig (device group): ") + ncclGetErrorString(r));
     }
     g_comms = cs;
@@ -326,7 +371,7 @@ struct DeviceGroup {
         }
     }
     ~DeviceGroup() {
-        if (vst) (void)hipStreamDestroy(vst);
+        if (vst) hip_quiet(hipStreamDestroy(vst));
     }
     int size() const { return (int)devs.size(); }
     // balanced rows: every shard non-empty
@@ -1168,9 +1213,9 @@ tritd_status tritd_dev_triple_product_f64(const double* A, const double* B, cons
         g.RP = padded_rank32(g.R);  // 16..256: the kernel is instantiated for every padded rank
         ScratchLease lease(st);
         ScratchSet& ss = lease.set();
-        double* Ah = scratch(ss, 0, (size_t)(g.n1p * g.RP));
-        double* Bh = scratch(ss, 1, (size_t)(n2 * g.RP));
-        double* ChT = scratch(ss, 2, (size_t)g.RP * g.n3p);
+        double* Ah = scratch(lease, 0, (size_t)(g.n1p * g.RP));
+        double* Bh = scratch(lease, 1, (size_t)(n2 * g.RP));
+        double* ChT = scratch(lease, 2, (size_t)g.RP * g.n3p);
         launch_pack_factors(g, A, B, C, Ah, Bh, ChT, st);
         launch_tp(g, Ah, Bh, ChT, X, nullptr, nullptr, 0, n1, n1 * n2, st);
         TRITD_HIP(hipEventRecord(ss.done, st));
@@ -1190,11 +1235,11 @@ tritd_status tritd_dev_triple_product_qi_f64(const double* A, const double* B, c
         g.RP = padded_rank32(g.R);
         ScratchLease lease(st);
         ScratchSet& ss = lease.set();
-        double* Ah = scratch(ss, 0, (size_t)(g.n1p * g.RP));
-        double* Bh = scratch(ss, 1, (size_t)(n2 * g.RP));
-        double* ChT = scratch(ss, 2, (size_t)g.RP * g.n3p);
-        double* H = scratch(ss, 3, (size_t)(g.n1p * n2 * g.RP));
-        double* ones = scratch(ss, 4, (size_t)g.RP);
+        double* Ah = scratch(lease, 0, (size_t)(g.n1p * g.RP));
+        double* Bh = scratch(lease, 1, (size_t)(n2 * g.RP));
+        double* ChT = scratch(lease, 2, (size_t)g.RP * g.n3p);
+        double* H = scratch(lease, 3, (size_t)(g.n1p * n2 * g.RP));
+        double* ones = scratch(lease, 4, (size_t)g.RP);
         launch_pack_factors(g, A, B, C, Ah, Bh, ChT, st);
         launch_fill(ones, g.RP, 1.0, st);
         launch_qi_h(g, r, Ah, Bh, H, nullptr, st);
@@ -1344,7 +1389,7 @@ tritd_status tritd_dev_evaluate_f64(const double* X, int64_t n, const double* gt
             out.alloc(2);
             int64_t* sc = nullptr;
             TRITD_HIP(hipMalloc(&sc, (size_t)(nb + 1) * sizeof(int64_t)));
-            struct Free { int64_t* p; ~Free() { (void)hipFree(p); } } fr{sc};
+            struct Free { int64_t* p; ~Free() { hip_quiet(hipFree(p)); } } fr{sc};
             launch_evaluate(X, gt, m, mask, n, sc, part.p, out.p, sc + nb, st);
             int64_t total = n;
             if (mask)

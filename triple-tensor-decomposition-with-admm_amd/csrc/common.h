@@ -19,13 +19,32 @@ struct Error : std::runtime_error {
     Error(tritd_status c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+// A HIP call that must succeed.  A call that returns success but leaves the
+// thread's last error set (hipGetLastError: sticky until read) is reported
+// here, by name, instead of at the next launch check (TRITD_CHECK_LAUNCH
+// reads that same state): with every HIP call of the library either checked
+// here or made through hip_quiet, and each entry point clearing the state it
+// inherits (api.cpp guarded), a launch check reports only its own launch.
 #define TRITD_HIP(expr)                                                                      \
     do {                                                                                     \
         hipError_t e_ = (expr);                                                              \
         if (e_ != hipSuccess)                                                                \
             throw ::tritd::Error(e_ == hipErrorOutOfMemory ? TRITD_ERR_NOMEM : TRITD_ERR_HIP, \
                                  std::string(#expr) + ": " + hipGetErrorString(e_));        \
+        e_ = hipPeekAtLastError();                                                           \
+        if (e_ != hipSuccess) {                                                              \
+            (void)hipGetLastError();                                                         \
+            throw ::tritd::Error(TRITD_ERR_HIP, std::string(#expr) +                         \
+                                                    " returned success but left the last "   \
+                                                    "error set: " + hipGetErrorString(e_));  \
+        }                                                                                    \
     } while (0)
+
+// A HIP call whose failure is deliberately ignored (destructors, cleanup
+// after an error): it must not leave the thread's last error behind either.
+inline void hip_quiet(hipError_t e) {
+    if (e != hipSuccess) (void)hipGetLastError();
+}
 
 // a launch's error, named by the launching site
 #define TRITD_STR2_(x) #x

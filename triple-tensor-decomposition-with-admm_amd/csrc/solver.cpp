@@ -183,7 +183,7 @@ Session::Session(int device, const void* D, int64_t ldD, int64_t n1, int64_t n2,
                     e = hipMemcpy2DAsync(dstage_.p, g_.n1l * es_, D, ldD * es_, g_.n1l * es_,
                                          (size_t)(n2 * n3), hipMemcpyHostToDevice, cs);
                 if (e == hipSuccess) e = hipStreamSynchronize(cs);
-                (void)hipStreamDestroy(cs);
+                hip_quiet(hipStreamDestroy(cs));
                 TRITD_HIP(e);
             };
         }
@@ -320,17 +320,17 @@ void Session::create_streams(hipStream_t shared_stream) {
 }
 
 Session::~Session() {
-    (void)hipSetDevice(device_);
-    if (st_) (void)hipStreamSynchronize(st_);
+    hip_quiet(hipSetDevice(device_));
+    if (st_) hip_quiet(hipStreamSynchronize(st_));
     if (side_) {
-        (void)hipStreamSynchronize(side_);
-        (void)hipStreamDestroy(side_);
+        hip_quiet(hipStreamSynchronize(side_));
+        hip_quiet(hipStreamDestroy(side_));
     }
     for (hipEvent_t e : {evAtA_, evBtB_, evCtC_, evSA_, evSB_, evSC_})
-        if (e) (void)hipEventDestroy(e);
-    for (auto e : ev_) (void)hipEventDestroy(e);
-    if (ctrl_) (void)hipFree(ctrl_);
-    if (own_stream_ && st_) (void)hipStreamDestroy(st_);
+        if (e) hip_quiet(hipEventDestroy(e));
+    for (auto e : ev_) hip_quiet(hipEventDestroy(e));
+    if (ctrl_) hip_quiet(hipFree(ctrl_));
+    if (own_stream_ && st_) hip_quiet(hipStreamDestroy(st_));
 }
 
 void Session::set_normD_from_red3() {
@@ -444,19 +444,24 @@ void Session::solve(int mode, const double* P, const double* Q, double alpha, do
         launch_solve(g_.RP, g_.R, G, ones_.p, alpha, out, ctrl_ + 2, ctrl_, s);
     }
     // the generic apply's pinv fallback, on the solve's stream (a side-stream
-    // solve then hands over a finished Ginv: one launch fewer on the main one)
-    if (gen_apply()) launch_pinv_fix(g_.RP, out, ctrl_, ctrl_ + 2, s);
+    // solve then hands over a finished Ginv: one launch fewer on the main one).
+    // Not for mode 0: solve A of iteration k+1 runs beside K5 of k, before k's
+    // stop test, and a fallback there could raise TRITD_FLAG_PINV_TOL for an
+    // update_A that MATLAB never performs when the loop stops at k (ADVICE
+    // r5); apply A runs the fallback itself, after the stop test (do_apply_A)
+    if (gen_apply() && mode != 0) launch_pinv_fix(g_.RP, out, ctrl_, ctrl_ + 2, s);
 }
 
 // (X*F')*pinv(G): fp64 path through the MFMA apply (RP <= 64); fp32
 // path single in, single-rounded out (MATLAB single * double = single)
 void Session::do_apply_A(double* Ginv) {
+    // (fix = true: the pinv fallback of solve A runs here, after the stop test)
     if (f32_)
         launch_apply_gen(g_.RP, nullptr, M1_.f(), g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
-                         true, ctrl_, ctrl_ + 2, st_, false);
+                         true, ctrl_, ctrl_ + 2, st_, true);
     else if (g_.RP > 64)  // fp64 r = 9..16
         launch_apply_gen(g_.RP, M1_.p, nullptr, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, nullptr,
-                         false, ctrl_, ctrl_ + 2, st_, false);
+                         false, ctrl_, ctrl_ + 2, st_, true);
     else
         launch_apply(g_.RP, M1_.p, g_.n1p, Ginv, Ah_.p, AhT_.p, g_.n1p, ctrl_, ctrl_ + 2, st_);
 }
@@ -910,13 +915,13 @@ double* Session::probe_pool(size_t pool_bytes, size_t slot, size_t stagger,
             enqueue_from(from);
             collect_from(from);
         }
-        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : ev) hip_quiet(hipEventDestroy(e));
     } else {
         probe_ms_.assign(cand.size(), 0.0);
     }
     if (overlap) overlap();  // (no probe ran)
     for (size_t c = 0; c < cand.size(); ++c)
-        if (c != best) (void)hipFree(cand[c]);
+        if (c != best) hip_quiet(hipFree(cand[c]));
     probe_pick_ = (int)best;
     return cand[best];
 }
@@ -1211,7 +1216,7 @@ void Session::harvest_timing() {
         ++acc_n_;
     }
     for (auto e : ev_)
-        if (e) (void)hipEventDestroy(e);
+        if (e) hip_quiet(hipEventDestroy(e));
     ev_.clear();
     ev_iter_.clear();
 }

@@ -46,7 +46,7 @@ struct DBuf {
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() {
-        if (p && owned) (void)hipFree(p);
+        if (p && owned) hip_quiet(hipFree(p));
     }
     void alloc(size_t count) {
         n = count;
@@ -54,7 +54,7 @@ struct DBuf {
     }
     void alloc_bytes(size_t bytes) { alloc((bytes + sizeof(double) - 1) / sizeof(double)); }
     void release() {
-        if (p && owned) (void)hipFree(p);
+        if (p && owned) hip_quiet(hipFree(p));
         p = nullptr;
         n = 0;
     }
