@@ -62,28 +62,46 @@ def ensure_built():
     subprocess.run(["make", "-j8", "-C", csrc], check=True, stdout=subprocess.DEVNULL)
 
 
-def cpu_baseline(D, r, opts, A0, B0, C0, iters):
-    """Time the C restatement of the reference on the host (bounded sample)."""
+def cpu_baseline(D, r, opts, A0, B0, C0, iters, Lstar=None):
+    """Time the C restatement of the reference on the host (BASELINE.md §3,
+    SURVEY.md §8d): every core the process may use (OMP_NUM_THREADS if set,
+    else the CPUs in this process's affinity mask), the CPU model recorded,
+    the full solve (100 iterations at configs 1-4), and — given the clean
+    tensor — the restatement's final RRE (traffic_triple_comparison.m:62-63,
+    evaluate :194-199), so the line carries |RRE_gpu - RRE_cpu| from this box."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         if not os.path.exists(os.path.join(ROOT, "oracle", "build", "libtritd_ref.so")):
             subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                            stdout=subprocess.DEVNULL)
+        import ctypes as C
         import tritd_ref
         lib = tritd_ref.load()
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        env_t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        threads = env_t or len(os.sched_getaffinity(0))
         lib.tritd_ref_set_threads(threads)
         t0 = time.perf_counter()
         out = tritd_ref.admm(lib, D, r, opts, A0, B0, C0, max_iters=iters)
         dt = time.perf_counter() - t0
         k = out[6]
         prec = "fp32 (MATLAB single rules)" if D.dtype == np.float32 else "fp64"
-        return {"value": k / dt, "unit": "iters/s", "cores": threads, "kind": "port",
-                "sample": "%d ADMM iterations of the same %dx%dx%d r=%d %s workload "
-                          "(C restatement of triple_decomp_ADMM.m with its materialised "
-                          "permutes/design matrices, GEMM and pinv; OpenMP; includes per-call "
-                          "setup)" % (k, *D.shape, r, prec),
-                "seconds": dt}
+        res = {"value": k / dt, "unit": "iters/s", "cores": threads,
+               "threads_from": "OMP_NUM_THREADS" if env_t else "sched_getaffinity",
+               "cpu_model": cpu_model(), "kind": "port", "iterations": k,
+               "sample": "%d ADMM iterations of the same %dx%dx%d r=%d %s workload "
+                         "(C restatement of triple_decomp_ADMM.m with its materialised "
+                         "permutes/design matrices, GEMM and pinv; OpenMP; includes per-call "
+                         "setup)" % (k, *D.shape, r, prec),
+               "seconds": dt, "rre": None, "k": k, "errHist_final": float(out[4][-1])}
+        if Lstar is not None:
+            n1, n2, n3 = D.shape
+            L = np.zeros((n1, n2, n3), order="F")
+            p = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+            A, B, Cc = (np.asfortranarray(x, dtype=np.float64) for x in out[:3])
+            lib.tritd_ref_triple_product(p(A), p(B), p(Cc), n1, n2, n3, r, p(L))
+            num = float(np.sum(np.square(L - Lstar)))
+            res["rre"] = float(np.sqrt(num) / np.linalg.norm(Lstar))
+        return res
     except Exception as e:  # the baseline is reported, never the product
         return {"value": None, "unit": "iters/s", "cores": 0, "kind": "port",
                 "sample": "unavailable: %s" % e}
@@ -224,57 +242,21 @@ def primitives(device, n=512, r=8, reps=10):
     return out
 
 
-def config5_leg(steps, warmup=2):
-    """`bench.py --config 5` for `steps` timed iterations in a child process
-    (its own device memory; host data generated there), reduced to the keys
-    that place it beside the config-4 line: iters/s, ms per iteration, K5
-    against the f32 MFMA peak, K2, final RRE."""
-    cmd = [sys.executable, os.path.abspath(__file__), "--config", "5", "--steps", str(steps),
-           "--warmup", str(warmup), "--no-cpu", "--no-e2e", "--no-prims", "--no-c5"]
-    t0 = time.perf_counter()
-    try:
-        p = subprocess.run(cmd, capture_output=True, text=True, timeout=480)
-    except subprocess.TimeoutExpired:
-        return {"error": "config-5 leg timed out (480 s)"}
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    if p.returncode != 0 or not lines:
-        return {"error": "config-5 leg failed (rc %d): %s" % (p.returncode, p.stderr[-500:])}
-    d = json.loads(lines[-1])
-    roof = d["roofline"]
-    return {"workload": d["config"]["workload"], "value": d["value"], "unit": d["unit"],
-            "ms_per_step": d["ms_per_step"], "steps": d["steps"], "warmup": d["warmup"],
-            "dtype": d["dtype"], "rre_final": d["rre_final"], "k_final": d["k_final"],
-            "fused_update_ms": d["kernel_ms"]["fused_update"],
-            "mode3_mttkrp_ms": d["kernel_ms"]["mode3_mttkrp"],
-            "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
-                                                  "kernel", "traffic", "traffic_source",
-                                                  "algorithmic_flops_per_launch")},
-            "mode3_mfma_frac": roof.get("mfma_gemm", {}).get("frac"),
-            "wall_s": round(time.perf_counter() - t0, 1)}
-
-
-def free_port():
+def listen_socket():
+    """rank 0's rendezvous socket (tritd.rendezvous.StarGroup): bound to an
+    ephemeral port on 127.0.0.1 and listening before any rank connects; the
+    rank-0 worker inherits the descriptor, so the port is never re-bound."""
     import socket
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    s.listen(64)
+    return s
 
 
-def spawn_ranks(n):
-    """`--gpus N > 1` without a torch.distributed launcher around us: start
-    the N rank processes ourselves, as CHILD processes (never an exec; this
-    process has not touched the GPU), with the environment torchrun would give
-    them (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT on 127.0.0.1).  Exit
-    code: 0 only if every rank exits 0; the first failure stops the rest."""
+def wait_all(procs):
+    """Exit code 0 only if every process exits 0; the first failure stops the
+    rest (a failed rank would leave the others in a collective)."""
     import signal
-    port = str(free_port())
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=port, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
     rc = 0
     live = list(procs)
     while live:
@@ -285,155 +267,151 @@ def spawn_ranks(n):
             live.remove(p)
             if c != 0 and rc == 0:
                 rc = c if c > 0 else 1
-                for q in live:  # a failed rank would leave the others in a collective
+                for q in live:
                     q.send_signal(signal.SIGTERM)
         time.sleep(0.05)
     return rc
 
 
+def worker_cmd():
+    return [sys.executable, os.path.abspath(__file__), "--worker"] + sys.argv[1:]
+
+
+def spawn_ranks(n):
+    """`--gpus N > 1` without a torch.distributed launcher around us: start
+    the N rank workers ourselves, as CHILD processes (never an exec; this
+    process has not touched the GPU), with torchrun's rank environment and
+    the rendezvous port; rank 0 inherits the listening socket."""
+    ls = listen_socket()
+    port = ls.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", TRITD_RDZV_PORT=str(port),
+                   OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+        fds = ()
+        if r == 0:
+            env["TRITD_RDZV_FD"] = str(ls.fileno())
+            fds = (ls.fileno(),)
+        procs.append(subprocess.Popen(worker_cmd(), env=env, pass_fds=fds))
+    ls.close()
+    return wait_all(procs)
+
+
+def rank_parent():
+    """A rank process started by torchrun (the driver's N > 1 launch): it
+    joins a gloo group on the CPU only to publish rank 0's rendezvous port,
+    then runs the rank's GPU work in a child worker that never imports torch
+    (so libtritd binds /opt/rocm's HIP runtime and RCCL, the stack the GPU
+    tests validate: VERDICT r5 next 3a), and exits with the worker's code.
+    This process never touches the GPU and never execs."""
+    import torch.distributed as tdist
+    rank = int(os.environ["RANK"])
+    tdist.init_process_group("gloo")
+    ls = listen_socket() if rank == 0 else None
+    port = [ls.getsockname()[1] if ls else None]
+    tdist.broadcast_object_list(port, src=0)
+    env = dict(os.environ, TRITD_RDZV_PORT=str(port[0]))
+    fds = ()
+    if ls is not None:
+        env["TRITD_RDZV_FD"] = str(ls.fileno())
+        fds = (ls.fileno(),)
+    p = subprocess.Popen(worker_cmd(), env=env, pass_fds=fds)
+    if ls is not None:
+        ls.close()
+    rc = wait_all([p])
+    try:
+        tdist.destroy_process_group()
+    except Exception:
+        pass
+    return rc
+
+
 def launch_check(args):
-    """--launch-check: the rank plumbing alone (gloo, no GPU): every rank joins
-    the process group, the ranks count themselves with an all-reduce, rank 0
-    prints one JSON line.  CPU test of the `--gpus N` spawn path."""
-    import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        dist.init_process_group("gloo")
-    t = torch.ones(1)
-    if world > 1:
-        dist.all_reduce(t)
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_counted": int(t.item()),
-                          "gpus_arg": args.gpus}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    """--launch-check: the rank plumbing alone (no GPU): every worker joins the
+    rendezvous, the ranks count themselves with an all-reduce, rank 0 prints
+    one JSON line.  CPU test of the `--gpus N` spawn and torchrun paths."""
+    from tritd.rendezvous import StarGroup
+    g = StarGroup.from_env(timeout=120)
+    n = g.allreduce_sum([1.0])[0]
+    torch_loaded = g.allgather("torch" in sys.modules)
+    if g.rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": g.world, "ranks_counted": int(n),
+                          "gpus_arg": args.gpus, "torch_in_workers": any(torch_loaded)}),
+              flush=True)
+    g.close()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=None, help="config 4: cube side override")
-    ap.add_argument("--r", type=int, default=None)
-    # bounded host sample: ~20 s at config 4, one iteration at config 5 (§8d)
-    ap.add_argument("--cpu-iters", type=int, default=None)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end one-shot calls")
-    ap.add_argument("--no-prims", action="store_true", help="skip the primitive kernels")
-    ap.add_argument("--no-c5", action="store_true",
-                    help="skip the config-5 leg of the default (config 4, N = 1) line")
-    ap.add_argument("--c5-steps", type=int, default=10, help="timed iterations of the config-5 leg")
-    ap.add_argument("--comm", default="rccl", choices=("rccl", "host"),
-                    help="N > 1: libtritd's RCCL communicator (default), or the host all-reduce "
-                         "transport over gloo (correctness rehearsal with ranks sharing a GPU)")
-    # --algo als: triple_decomp_ALS.m on the config-4 workload (SURVEY.md §8f rank 2)
-    ap.add_argument("--algo", default="admm", choices=("admm", "als"))
-    ap.add_argument("--launch-check", action="store_true",
-                    help="test the N-rank launch only (gloo, no GPU work)")
-    args = ap.parse_args()
-    if args.gpus < 1:
-        raise SystemExit("--gpus must be >= 1")
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # never a silent one-rank run of an N-GPU request
-        return spawn_ranks(args.gpus)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        raise SystemExit("--gpus %d does not match WORLD_SIZE %d" % (args.gpus, world))
-    if args.launch_check:
-        return launch_check(args)
-    if args.algo == "als":
-        if world > 1:
-            raise SystemExit("--algo als runs on one GPU")
-        return bench_als(args)
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    host_comm = args.comm == "host"
 
-    dist = None
-    if world > 1:
-        # torch only where ranks need torch.distributed (imported before
-        # tritd, so libtritd binds torch's HIP runtime: one per process); one
-        # GPU runs without torch, on /opt/rocm's runtime (tritd._lib)
-        import torch
-        import torch.distributed as dist
-        if host_comm:
-            # rehearsal of the N > 1 path on fewer GPUs than ranks: gloo for
-            # torch.distributed, libtritd's host all-reduce transport, ranks
-            # sharing devices round-robin (the timing is not a scaling number)
-            local_rank = local_rank % max(torch.cuda.device_count(), 1)
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        else:
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", rank=rank, world_size=world)
+def make_data(config, n1, n2, n3, r, rows):
+    """Synthetic inputs of `config`, rows = this rank's
+    mode-1 range; returns (D, Lstar, A0, B0, C0) with D / Lstar of those rows."""
+    from tritd import synth
+    i0, i1 = rows
+    if config == 2:  # RRE against the complete readings (traffic_triple_comparison.m:62)
+        d = synth.sensor_like(n1, n2, n3, r, missing=0.10, seed=0, init_seed=123)
+        d["Lstar"] = d.pop("X")
+    elif config == 3:  # RRE of the low-rank part against the frames
+        d = synth.video_like(n1, n2, n3, r, seed=0, init_seed=123)
+        d["Lstar"] = d.pop("X")
+    elif CONFIGS[config][4] == "f32":  # config 5: rounded to single, this rank's rows only
+        d = synth.low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123,
+                                             rows=rows)
+        return d["D"], d["Lstar"], d["A0"], d["B0"], d["C0"]
+    else:
+        d = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    D = np.asfortranarray(d["D"][i0:i1], dtype=np.float64)
+    L = np.asfortranarray(d["Lstar"][i0:i1], dtype=np.float64)
+    return D, L, d["A0"], d["B0"], d["C0"]
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
 
-    # one rank checks / rebuilds the library, the others wait for it (ranks
-    # building concurrently would race on the same objects)
-    if local_rank == 0:
-        ensure_built()
-    barrier()
+def run_case(config, K, W, group, comm, local_rank, n=None, r=None, host_comm=False):
+    """One sharded (or single-GPU) run of `config`: W untimed warm-up
+    iterations, K timed iterations between barriers (max over ranks), a K5
+    events pass, an events sample, then the untimed rest of the 100-iteration
+    solve and the driver's RRE.  Returns (result dict, (D, Lstar, A0, B0, C0))
+    — the data of this rank's rows, for the rank-0 extras."""
     import tritd
     from tritd import hip, synth
-    from tritd._lib import HIP_RUNTIME
-
-    n1, n2, n3, r, dts = CONFIGS[args.config]
-    if args.n is not None:
-        if args.config != 4:
-            raise SystemExit("--n applies to config 4 (n^3)")
-        n1 = n2 = n3 = args.n
-    r = args.r if args.r is not None else r
+    from tritd.dist import shard_bounds
+    world = group.world if group else 1
+    rank = group.rank if group else 0
+    n1, n2, n3, rr, dts = CONFIGS[config]
+    if n is not None:
+        n1 = n2 = n3 = n
+    rr = r if r is not None else rr
     f32 = dts == "f32"
     npdt = np.float32 if f32 else np.float64
-    cpu_iters = args.cpu_iters if args.cpu_iters is not None else (1 if f32 else 40)
-    K, W = args.steps, args.warmup
     maxIter = max(100, K + W)
-    base_opts = synth.VIDEO_OPTS if args.config == 3 else synth.TRAFFIC_OPTS
+    base_opts = synth.VIDEO_OPTS if config == 3 else synth.TRAFFIC_OPTS
     opts = dict(base_opts, maxIter=maxIter, tol=base_opts["tol"])
-    if args.config == 2:  # RRE against the complete readings (traffic_triple_comparison.m:62)
-        data = synth.sensor_like(n1, n2, n3, r, missing=0.10, seed=0, init_seed=123)
-        data["Lstar"] = data.pop("X")
-    elif args.config == 3:  # RRE of the low-rank part against the frames
-        data = synth.video_like(n1, n2, n3, r, seed=0, init_seed=123)
-        data["Lstar"] = data.pop("X")
-    elif f32:  # config 5: the same recipe, rounded to single (SURVEY.md §8d), streamed
-        data = synth.low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
-    else:
-        data = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
-    D, Lstar = data["D"].astype(npdt, order="F"), data["Lstar"].astype(npdt, order="F")
-    del data["D"], data["Lstar"]
-
-    # mode-1 shard of this rank
-    from tritd.dist import make_comm, make_host_comm, shard_bounds
     i0, i1 = shard_bounds(n1, world, rank)
-    comm = None
-    if world > 1:
-        comm = (make_host_comm if host_comm else make_comm)(dist, rank, world, local_rank)
-    # what the library's communicator itself reports (RCCL: ncclCommCount)
-    comm_info = comm.info() if comm is not None else (1, 0, "none")
-    if comm is not None and comm_info[0] != world:
-        raise SystemExit("communicator reports %d ranks, WORLD_SIZE is %d" % (comm_info[0], world))
+    D, Lstar, A0, B0, C0 = make_data(config, n1, n2, n3, rr, (i0, i1))
+
+    def barrier():
+        if group:
+            group.barrier()
 
     # inputs resident in HBM before the timed region
     hip.set_device(local_rank)
-    D_shard = hip.DeviceArray.from_host(np.asfortranarray(D[i0:i1]))
-    sess = tritd.Session(r, opts, data["A0"], data["B0"], data["C0"], n1=n1, n2=n2, n3=n3, i0=i0,
-                         i1=i1, d_device_ptr=D_shard.ptr, ldD=i1 - i0, device=local_rank,
-                         comm=comm, dtype=npdt)
+    D_shard = hip.DeviceArray.from_host(np.asfortranarray(D, dtype=npdt))
+    sess = tritd.Session(rr, opts, A0, B0, C0, n1=n1, n2=n2, n3=n3, i0=i0, i1=i1,
+                         d_device_ptr=D_shard.ptr, ldD=i1 - i0, device=local_rank, comm=comm,
+                         dtype=npdt)
     D_shard.free()
-
     sess.run(W)
     sess.sync()
     dense0, tiles_per_launch = sess.counters()
-    # host-side collectives of the bench itself (gloo wants CPU tensors)
-    cdev = (torch.device("cpu") if host_comm else torch.device("cuda", local_rank)) if dist else None
 
     def timed(k):
         barrier()
@@ -444,10 +422,8 @@ def main():
         hip.synchronize()
         barrier()
         dt = time.perf_counter() - t0
-        if dist is not None:
-            t = torch.tensor([dt], device=cdev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
+        if group:
+            dt = group.allreduce_max(dt)
         return dt, done, stopped
 
     # the timed region: K steps with no events (an event record is a stream
@@ -468,7 +444,6 @@ def main():
     probe_ms, probe_pick = sess.probe()
     if stopped:
         raise SystemExit("stop test fired inside the K5 events pass (k=%d)" % done)
-
     # K2 and whole-iteration event timings: an untimed sample right after the
     # timed region (the solve continues; events around every kernel there)
     n_more = min(10, maxIter - done)
@@ -485,26 +460,20 @@ def main():
     # completion on the session stream, waiting for the slowest rank
     # included) and the rest of the iteration (this rank's compute)
     per_rank = None
-    if dist is not None:
-        mine = torch.tensor([rank, i1 - i0, km["iteration"], ar_ms, ar_n, km["fused_update"]],
-                            dtype=torch.float64, device=cdev)
-        allv = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allv, mine)
+    if group and world > 1:
+        allv = group.allgather([rank, i1 - i0, km["iteration"], ar_ms, ar_n, km["fused_update"]])
         per_rank = [{"rank": int(v[0]), "rows": int(v[1]), "iteration_ms": float(v[2]),
                      "allreduce_ms": float(v[3]), "allreduces_per_iteration": int(v[4]),
                      "compute_ms": float(v[2] - v[3]), "fused_update_ms": float(v[5])}
-                    for v in (t.cpu() for t in allv)]
-
+                    for v in allv]
     # finish the solve (untimed) and report the driver RRE at the final k
     sess.run(maxIter - done)
     k_final, _ = sess.sync()
-    L_shard = hip.DeviceArray.from_host(np.asfortranarray(Lstar[i0:i1]))
+    L_shard = hip.DeviceArray.from_host(np.asfortranarray(Lstar, dtype=npdt))
     num, den = sess.rre_parts(L_shard.ptr, i1 - i0)
     L_shard.free()
-    if dist is not None:
-        t = torch.tensor([num, den], device=cdev, dtype=torch.float64)
-        dist.all_reduce(t)
-        num, den = float(t[0]), float(t[1])
+    if group and world > 1:
+        num, den = group.allreduce_sum([num, den])
     rre = float(np.sqrt(num / den))
     res = sess.get()
     errhist_final = float(res["errHist"][-1]) if len(res["errHist"]) else None
@@ -524,16 +493,16 @@ def main():
     # (dense-E mode, sess.k5_profile() = (7, 0): every E access is a dense stream)
     k5_bytes = int(streams * N_local * s_b + slots * tiles_per_launch * 256
                    + (max(slots - 1, 0) * dense_per_launch * tile_b if slots else 0)
-                   + r * r * nl * n2 * s_b)
+                   + rr * rr * nl * n2 * s_b)
     # flops: L(ij,t) = sum_k (Ah*Bh)(ij,k) Ch(t,k) and W = T x3 Ch, 2 N R each
-    k5_flops = 4.0 * N_local * r * r
+    k5_flops = 4.0 * N_local * rr * rr
     k5_ms = km["fused_update"]
     gbs = k5_bytes / (k5_ms * 1e-3) / 1e9 if k5_ms > 0 else None
     tfs = k5_flops / (k5_ms * 1e-3) / 1e12 if k5_ms > 0 else None
     # the committed PMC pass is of the 1-GPU launch (a shard moves 1/N of it)
     # (committed PMC passes exist for configs 4 and 5 at their default shapes)
-    pmc_ok = world == 1 and args.config in (4, 5) and args.n is None and args.r is None
-    traffic, traffic_src = pmc_traffic(args.config) if pmc_ok else (None, None)
+    pmc_ok = world == 1 and config in (4, 5) and n is None and r is None
+    traffic, traffic_src = pmc_traffic(config) if pmc_ok else (None, None)
     if f32:  # config 5 is MFMA-bound
         roof = {"bound": "mfma", "achieved": tfs, "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": (tfs / F32_MFMA_PEAK_TFS) if tfs else None,
@@ -548,96 +517,231 @@ def main():
                  "traffic_source": traffic_src, "algorithmic_bytes_per_launch": k5_bytes,
                  "e_dense_tiles_per_launch": dense_per_launch,
                  "e_tiles_per_launch": tiles_per_launch})
-
     # K2 (the mode-3 MTTKRP, X3*H' of :93): the RPAS GEMM north_star prices
     # against the MFMA peak; 2 * N_local * R flops per launch
     k2_ms = km["mode3"]
-    k2_flops = 2.0 * N_local * r * r
+    k2_flops = 2.0 * N_local * rr * rr
     k2_tfs = k2_flops / (k2_ms * 1e-3) / 1e12 if k2_ms > 0 else None
     k2_peak = F32_MFMA_PEAK_TFS if f32 else F64_MFMA_PEAK_TFS
-    pmc_util, pmc_src = pmc_mfma_util(args.config) if pmc_ok else (None, None)
+    pmc_util, pmc_src = pmc_mfma_util(config) if pmc_ok else (None, None)
     roof["mfma_gemm"] = {"kernel": "k_m3_cp (mode-3 MTTKRP, X3*H' of triple_decomp_ADMM.m:93)",
                          "achieved": k2_tfs, "peak": k2_peak, "unit": "TFLOP/s",
                          "frac": (k2_tfs / k2_peak) if k2_tfs else None,
                          "algorithmic_flops_per_launch": k2_flops, "ms": k2_ms,
                          "pmc_mfma_util": pmc_util, "pmc_source": pmc_src}
-
     sess.close()
+    out = {
+        "value": K / dt, "ms_per_step": dt * 1e3 / K, "steps": K, "warmup": W, "dtype": dts,
+        "n1": n1, "n2": n2, "n3": n3, "r": rr, "maxIter": maxIter, "opts": opts,
+        "workload": (WORKLOADS[config] if n is None and r is None
+                     else "config %d shape override: %dx%dx%d r=%d"
+                     % (config, n1, n2, n3, rr)).replace("%%", "%"),
+        "per_rank": per_rank, "rre_final": rre, "k_final": k_final,
+        "errHist_final": errhist_final,
+        "kernel_ms": {"fused_update": k5_ms, "mode3_mttkrp": km["mode3"],
+                      "iteration_events": km["iteration"], "samples": km["samples"],
+                      "k5_events_pass": {"steps": K2n, "ms_per_step": dt_ev * 1e3 / K2n,
+                                         "note": "a second timed pass with HIP events "
+                                                 "around K5 only (value is the pass "
+                                                 "without events)"}},
+        "roofline": roof,
+        "placement_probe": {"ms": [round(m, 4) for m in probe_ms], "picked": probe_pick},
+    }
+    return out, (D, Lstar, A0, B0, C0)
+
+
+def c5_reference():
+    """The committed 100-iteration class-single restatement of config 5
+    (tests/golden/c5_horizon.npz, tests/golden/make_c5_horizon.py), or None."""
+    f = os.path.join(ROOT, "tests", "golden", "c5_horizon.npz")
+    if not os.path.exists(f):
+        return None
+    z = np.load(f)
+    return {"k": int(z["k"]), "rre": float(z["rre"]), "errHist_final": float(z["errHist"][-1]),
+            "source": os.path.relpath(f, ROOT)}
+
+
+def config5_summary(d):
+    """The keys that place config 5 beside the config-4 line, plus its RRE
+    against the committed full-horizon CPU restatement."""
+    roof = d["roofline"]
+    out = {"workload": d["workload"], "value": d["value"], "unit": "iters/s",
+           "ms_per_step": d["ms_per_step"], "steps": d["steps"], "warmup": d["warmup"],
+           "dtype": d["dtype"], "rre_final": d["rre_final"], "k_final": d["k_final"],
+           "errHist_final": d["errHist_final"],
+           "fused_update_ms": d["kernel_ms"]["fused_update"],
+           "mode3_mttkrp_ms": d["kernel_ms"]["mode3_mttkrp"],
+           "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac",
+                                                 "kernel", "traffic", "traffic_source",
+                                                 "algorithmic_flops_per_launch")},
+           "mode3_mfma_frac": roof.get("mfma_gemm", {}).get("frac"),
+           "per_rank": d["per_rank"]}
+    ref = c5_reference()
+    if ref is not None and d["maxIter"] == 100:
+        out["cpu_restatement"] = ref
+        out["rre_vs_cpu"] = abs(d["rre_final"] - ref["rre"])
+        out["rre_bound"] = 1e-6 + 2e-5 * ref["rre"]
+        out["k_matches_cpu"] = d["k_final"] == ref["k"]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None, help="config 4: cube side override")
+    ap.add_argument("--r", type=int, default=None)
+    # BASELINE.md §3: the full 100-iteration solve at configs 1-4 (one
+    # iteration at config 5, reported per iteration)
+    ap.add_argument("--cpu-iters", type=int, default=None)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end one-shot calls")
+    ap.add_argument("--no-prims", action="store_true", help="skip the primitive kernels")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the config-5 leg of the default (config 4) line")
+    ap.add_argument("--c5-steps", type=int, default=10, help="timed iterations of the config-5 leg")
+    ap.add_argument("--comm", default="rccl", choices=("rccl", "host"),
+                    help="N > 1: libtritd's RCCL communicator (default), or the host all-reduce "
+                         "transport over the rendezvous sockets (correctness rehearsal with ranks "
+                         "sharing a GPU)")
+    # --algo als: triple_decomp_ALS.m on the config-4 workload (SURVEY.md §8f rank 2)
+    ap.add_argument("--algo", default="admm", choices=("admm", "als"))
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test the N-rank launch only (rendezvous, no GPU work)")
+    ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # never a silent one-rank run of an N-GPU request
+        return spawn_ranks(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d does not match WORLD_SIZE %d" % (args.gpus, world))
+    if world > 1 and not args.worker:
+        return rank_parent()  # started by torchrun: GPU work in a torch-free child
+    if args.launch_check:
+        return launch_check(args)
+    if args.algo == "als":
+        if world > 1:
+            raise SystemExit("--algo als runs on one GPU")
+        return bench_als(args)
+
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    host_comm = args.comm == "host"
+    group = None
+    if world > 1:
+        from tritd.rendezvous import StarGroup
+        group = StarGroup.from_env()
+
+    # one rank checks / rebuilds the library, the others wait for it (ranks
+    # building concurrently would race on the same objects)
+    if local_rank == 0:
+        ensure_built()
+    if group:
+        group.barrier()
+    import tritd
+    from tritd import hip
+    from tritd._lib import HIP_RUNTIME, hip_runtimes, runtime_stack
+
+    comm = None
+    if world > 1:
+        from tritd.rendezvous import make_comm, make_host_comm
+        if host_comm:
+            # rehearsal of the N > 1 path on fewer GPUs than ranks (the
+            # timing is not a scaling number)
+            local_rank = local_rank % max(tritd.device_count(), 1)
+            comm = make_host_comm(group, local_rank)
+        else:
+            comm = make_comm(group, local_rank)
+    # what the library's communicator itself reports (RCCL: ncclCommCount)
+    comm_info = comm.info() if comm is not None else (1, 0, "none")
+    if comm is not None and comm_info[0] != world:
+        raise SystemExit("communicator reports %d ranks, WORLD_SIZE is %d" % (comm_info[0], world))
+
+    main_res, data = run_case(args.config, args.steps, args.warmup, group, comm, local_rank,
+                              n=args.n, r=args.r, host_comm=host_comm)
+    D, Lstar, A0, B0, C0 = data
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = end_to_end(tritd, D, r, opts, data["A0"], data["B0"], data["C0"], local_rank)
-
+        e2e = end_to_end(tritd, D, main_res["r"], main_res["opts"], A0, B0, C0, local_rank)
     prims = None
     if rank == 0 and world == 1 and not args.no_prims:
         prims = primitives(local_rank)
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(D, r, opts, data["A0"], data["B0"], data["C0"], cpu_iters)
+        f32 = CONFIGS[args.config][4] == "f32"
+        iters = args.cpu_iters if args.cpu_iters is not None else (1 if f32 else 100)
+        cpu = cpu_baseline(D, main_res["r"], main_res["opts"], A0, B0, C0, iters,
+                           Lstar=None if f32 else Lstar)
+    del D, Lstar, data
 
-    # the north_star's second headline configuration in the same line
-    # (VERDICT r4 next 5): a bounded config-5 run in a child process, after
-    # this process has released its device memory
+    # the north_star's second headline configuration in the same line (VERDICT
+    # r4 next 5, r5 next 3b): a bounded config-5 run on the same ranks and
+    # communicator, after the config-4 session has released its device memory
     c5 = None
-    if (rank == 0 and world == 1 and args.config == 4 and args.n is None and args.r is None
-            and not args.no_c5):
-        c5 = config5_leg(args.c5_steps)
+    if args.config == 4 and args.n is None and args.r is None and not args.no_c5:
+        d5, _ = run_case(5, args.c5_steps, 2, group, comm, local_rank, host_comm=host_comm)
+        c5 = config5_summary(d5)
 
     if rank == 0:
         line = {
             "metric": "ADMM iters/sec + final RRE, 512^3 r=8 tensor at 1/2/4/8 MI355X",
-            "value": K / dt,
+            "value": main_res["value"],
             "unit": "iters/s",
             "n_gpus": world,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": dt * 1e3 / K,
+            "steps": main_res["steps"],
+            "warmup": main_res["warmup"],
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": dts,
+            "dtype": main_res["dtype"],
             "data": "synthetic",
-            "config": {"workload": (WORKLOADS[args.config] if args.n is None and args.r is None
-                                    else "config %d shape override: %dx%dx%d r=%d"
-                                    % (args.config, n1, n2, n3, r)).replace("%%", "%"),
-                       "n1": n1, "n2": n2, "n3": n3, "r": r, "maxIter": maxIter,
+            "config": {"workload": main_res["workload"],
+                       "n1": main_res["n1"], "n2": main_res["n2"], "n3": main_res["n3"],
+                       "r": main_res["r"], "maxIter": main_res["maxIter"],
                        "parallelism": "mode1-shard x%d" % world
                                       + (" (host all-reduce rehearsal: not a scaling number)"
                                          if host_comm and world > 1 else "")},
             "comm": {"transport": comm_info[2], "nranks": comm_info[0]},
-            # the libamdhip64 libtritd ran on (/opt/rocm's without torch)
+            # the libamdhip64 libtritd ran on (/opt/rocm's: no rank imports torch)
             "hip_runtime": HIP_RUNTIME,
+            "hip_runtimes_mapped": len(hip_runtimes()),
+            # HIP / HSA / RCCL copies mapped in rank 0 (one each, /opt/rocm)
+            "runtime_stack": runtime_stack(),
             "rccl_nranks": comm_info[0] if comm_info[2] == "rccl" else None,
             # N > 1: per rank, from an events sample after the timed region
-            "per_rank": per_rank,
-            "rre_final": rre,
-            "k_final": k_final,
-            "errHist_final": errhist_final,
-            "kernel_ms": {"fused_update": k5_ms, "mode3_mttkrp": km["mode3"],
-                          "iteration_events": km["iteration"], "samples": km["samples"],
-                          "k5_events_pass": {"steps": K2n, "ms_per_step": dt_ev * 1e3 / K2n,
-                                             "note": "a second timed pass with HIP events "
-                                                     "around K5 only (value is the pass "
-                                                     "without events)"}},
-            "roofline": roof,
+            "per_rank": main_res["per_rank"],
+            "rre_final": main_res["rre_final"],
+            # |RRE_gpu - RRE_cpu| on this box (BASELINE.md §3, SURVEY.md §8d)
+            "rre_vs_cpu": (abs(main_res["rre_final"] - cpu["rre"])
+                           if cpu and cpu.get("rre") is not None else None),
+            "k_final": main_res["k_final"],
+            "errHist_final": main_res["errHist_final"],
+            "kernel_ms": main_res["kernel_ms"],
+            "roofline": main_res["roofline"],
             "cpu_baseline": cpu,
             # candidate tensor pools timed with K5's access pattern at session
-            # creation (rank 0), the fastest kept
-            "placement_probe": {"ms": [round(m, 4) for m in probe_ms], "picked": probe_pick},
+            # creation (rank 0), the fastest kept (DESIGN.md §3)
+            "placement_probe": main_res["placement_probe"],
             # one whole triple_decomp_ADMM call (maxIter=100), host arrays in and out,
             # timed like the drivers' tic/toc (traffic_triple_comparison.m:51,61)
             "end_to_end": e2e,
             # unfold / soft_threshold / triple_product on 512^3 fp64, device-resident
             "primitives": prims,
-            # config 5 (2048x2048x256 fp32 r=16), a bounded run of its own
+            # config 5 (2048x2048x256 fp32 r=16) on the same ranks, a bounded run
             "config5": c5,
         }
         print(json.dumps(line), flush=True)
 
     if comm is not None:
         comm.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if group is not None:
+        group.close()
 
 
 def cpu_baseline_als(X, r, A0, B0, C0, iters):

@@ -239,6 +239,9 @@ def test_hip_runtime_with_torch_imported_first_is_torch_s():
     m = _maps("torch_first")
     assert len(m["hip"]) == 1 and "torch" in m["hip"][0], m
     assert m["bound"] == m["hip"][0]
+    # one HSA runtime and one RCCL too: libtritd's
+    # ncclCommInitRank runs on whichever RCCL torch mapped
+    assert len(m["hsa"]) == 1 and len(m["rccl"]) == 1, m
 
 
 def test_torch_imported_after_tritd_fails_loudly():

@@ -1,7 +1,8 @@
 """bench.py's multi-rank launch (VERDICT r3 "next" 1): `--gpus N` from a plain
 shell must run N rank processes itself, or fail; never a silent 1-rank line.
 
-CPU tests run the launcher with `--launch-check` (gloo, no GPU work); the GPU
+CPU tests run the launcher with `--launch-check` (the rendezvous alone, no GPU
+work), from a plain shell and under torchrun; the GPU
 test runs the real sharded bench with 2 ranks sharing the box's one GPU
 through the library's host all-reduce transport (RCCL refuses one GPU twice)."""
 import json
@@ -36,6 +37,26 @@ def test_gpus_n_spawns_n_ranks(n):
     assert lines[0]["n_gpus"] == n and lines[0]["ranks_counted"] == n
 
 
+def test_torchrun_launch_runs_torch_free_workers():
+    """The driver's N > 1 launch (`python -m torch.distributed.run ...
+    bench.py --gpus N`): each torchrun rank joins gloo on the CPU only to
+    publish rank 0's rendezvous port and runs its work in a child that never
+    imports torch (tritd.rendezvous)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), BENCH, "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_counted"] == 2
+    assert lines[0]["torch_in_workers"] is False
+
+
 def test_world_size_mismatch_fails_loudly():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"],
                        capture_output=True, text=True, timeout=120, env=_env(WORLD_SIZE="1"))
@@ -62,6 +83,7 @@ def test_bench_two_ranks_from_plain_shell():
     line = lines[0]
     assert line["n_gpus"] == 2
     assert line["comm"] == {"transport": "host", "nranks": 2}
+    assert line["hip_runtimes_mapped"] == 1 and "/opt/rocm" in line["hip_runtime"]
     assert line["value"] > 0 and line["rre_final"] < 1e-3
     # the per-rank breakdown: each rank's rows, iteration,
     # all-reduce and compute ms, two all-reduces per iteration

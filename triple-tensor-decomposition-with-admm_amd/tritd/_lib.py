@@ -139,13 +139,27 @@ def _torch_lib_dir():
     return os.path.join(list(spec.submodule_search_locations)[0], "lib")
 
 
-def hip_runtimes():
-    """Distinct libamdhip64 files mapped into this process (/proc/self/maps)."""
+def mapped_libraries(stem):
+    """Distinct files whose name starts with `stem` mapped into this process
+    (/proc/self/maps), e.g. "libamdhip64", "libhsa-runtime64", "librccl"."""
     try:
         maps = open("/proc/self/maps").read()
     except OSError:
         return []
-    return sorted(set(re.findall(r"(/\S*libamdhip64\S*)", maps)))
+    return sorted(set(re.findall(r"(/\S*/%s\S*)" % re.escape(stem), maps)))
+
+
+def hip_runtimes():
+    """Distinct libamdhip64 files mapped into this process (/proc/self/maps)."""
+    return mapped_libraries("libamdhip64")
+
+
+def runtime_stack():
+    """The HIP runtime, HSA runtime and RCCL copies this process has mapped:
+    exactly one of each, from /opt/rocm, unless torch was imported first."""
+    return {k: mapped_libraries(v) for k, v in (("hip", "libamdhip64"),
+                                                 ("hsa", "libhsa-runtime64"),
+                                                 ("rccl", "librccl"))}
 
 
 def _preload_hip_runtime():

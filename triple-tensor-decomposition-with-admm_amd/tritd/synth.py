@@ -76,7 +76,8 @@ def low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123, mod
     return dict(D=D, Lstar=Lstar, A0=A0, B0=B0, C0=C0)
 
 
-def low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123, chunk=64):
+def low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123, chunk=64,
+                               rows=None):
     """low_rank_plus_outliers(...) rounded to single (D and L* as float32,
     column-major) without its fp64 full-size temporaries: the same draws from
     the same generator streams, produced in chunks of mode-1 rows (the support
@@ -85,8 +86,16 @@ def low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123,
     one-shot recipe's second call starts).  Equal to
     `low_rank_plus_outliers(...)["D"].astype(np.float32)` except where
     sigma = std(L*), summed chunk-wise here, differs in its last fp64 bit
-    (config 5: 2048x2048x256 in ~10 GB instead of ~35 GB)."""
+    (config 5: 2048x2048x256 in ~10 GB instead of ~35 GB).
+
+    rows=(i0, i1): only the mode-1 rows i0..i1-1 of D and L* (a rank's shard,
+    SURVEY.md §8e), identical to those rows of the full call: sigma still
+    comes from every row of L* (computed, not kept), and both draw streams are
+    advanced past the rows before i0 (one 64-bit draw per value, PCG64)."""
     import copy
+    i0, i1 = (0, n1) if rows is None else (int(rows[0]), int(rows[1]))
+    if not 0 <= i0 < i1 <= n1:
+        raise ValueError("rows must satisfy 0 <= i0 < i1 <= n1")
     rng = np.random.default_rng(seed)
     As = np.asfortranarray(rng.standard_normal((n1, r, r)))
     Bs = np.asfortranarray(rng.standard_normal((r, n2, r)))
@@ -94,13 +103,13 @@ def low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123,
     Ah, Bh, Ch = hat_factors(As, Bs, Cs)
     R = Ah.shape[1]
     KR = (Bh[:, None, :] * Ch[None, :, :]).reshape((n2 * n3, R), order="F")
-    L = np.empty((n1, n2, n3), dtype=np.float32, order="F")
+    L = np.empty((i1 - i0, n2, n3), dtype=np.float32, order="F")
     # std(L*) in one pass: per-chunk mean and centred sum of squares,
     # combined pairwise (Chan, Golub & LeVeque)
     cnt, mean, m2 = 0, 0.0, 0.0
-    for i0 in range(0, n1, chunk):
-        i1 = min(n1, i0 + chunk)
-        blk = (Ah[i0:i1] @ KR.T).reshape((i1 - i0, n2, n3), order="F")
+    for c0 in range(0, n1, chunk):
+        c1 = min(n1, c0 + chunk)
+        blk = (Ah[c0:c1] @ KR.T).reshape((c1 - c0, n2, n3), order="F")
         nb = blk.size
         mb = float(blk.mean())
         m2b = float(np.square(blk - mb).sum())
@@ -109,21 +118,26 @@ def low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123,
         mean += delta * nb / tot
         m2 += m2b + delta * delta * cnt * nb / tot
         cnt = tot
-        L[i0:i1] = blk
+        lo, hi = max(c0, i0), min(c1, i1)
+        if lo < hi:
+            L[lo - i0:hi - i0] = blk[lo - c0:hi - c0]
     sigma = float(np.sqrt(m2 / cnt))
     N = n1 * n2 * n3
+    skip = i0 * n2 * n3
     rs = rng
     bg = copy.deepcopy(rng.bit_generator)
-    bg.advance(N)
+    bg.advance(N + skip)
     rv = np.random.Generator(bg)
-    D = np.empty((n1, n2, n3), dtype=np.float32, order="F")
-    for i0 in range(0, n1, chunk):
-        i1 = min(n1, i0 + chunk)
-        c = i1 - i0
+    if skip:
+        rs.bit_generator.advance(skip)
+    D = np.empty((i1 - i0, n2, n3), dtype=np.float32, order="F")
+    for c0 in range(i0, i1, chunk):
+        c1 = min(i1, c0 + chunk)
+        c = c1 - c0
         sup = rs.random((c, n2, n3)) < p_out
         vals = rv.uniform(-10.0 * sigma, 10.0 * sigma, size=(c, n2, n3))
-        blk = (Ah[i0:i1] @ KR.T).reshape((c, n2, n3), order="F")
-        D[i0:i1] = blk + np.where(sup, vals, 0.0)
+        blk = (Ah[c0:c1] @ KR.T).reshape((c, n2, n3), order="F")
+        D[c0 - i0:c1 - i0] = blk + np.where(sup, vals, 0.0)
     A0, B0, C0 = random_factors(n1, n2, n3, r, init_seed)
     return dict(D=D, Lstar=L, A0=A0, B0=B0, C0=C0)
 
