@@ -207,3 +207,20 @@ def sample_L(A, B, Cc, idx):
     j = (idx // n1) % n2
     t = idx // (n1 * n2)
     return np.einsum("sk,sk,sk->s", Ah[i], Bh[j], Ch[t])
+
+
+def diff_parts(A, B, Cc, A2, B2, C2):
+    """(||L - L2||^2, ||L2||^2) for L = triple_product(A,B,C), L2 =
+    triple_product(A2,B2,C2), formed in double one frontal slice at a time:
+    L(:,:,t) - L2(:,:,t) = [A^.*C^(t,:), A2^.*C2^(t,:)] [B^, -B2^]' (one GEMM)."""
+    Ah, Bh, Ch = hat(A, B, Cc)
+    Ah2, Bh2, Ch2 = hat(A2, B2, C2)
+    Bcat = np.concatenate([Bh, -Bh2], axis=1)
+    num = den = 0.0
+    for t in range(Ch.shape[0]):
+        Acat = np.concatenate([Ah * Ch[t], Ah2 * Ch2[t]], axis=1)
+        dlt = Bcat @ Acat.T
+        l2 = Bh2 @ (Ah2 * Ch2[t]).T
+        num += float(np.vdot(dlt, dlt))
+        den += float(np.vdot(l2, l2))
+    return num, den

@@ -67,7 +67,10 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 static constexpr int K5_WAVES = 4;
 // Waves per SIMD at RP <= 64 (VGPR + AGPR <= 256).  One wave per SIMD: 1.243
 // vs 0.998 ms (round 2); three need <= 168 VGPRs and spill.
-static constexpr int K5_WPE = 2;
+#ifndef TRITD_K5_WPE
+#define TRITD_K5_WPE 2
+#endif
+static constexpr int K5_WPE = TRITD_K5_WPE;
 // Nontemporal hint (buffer aux bit 1) on the streamed tensors, loads and
 // stores: round 2 interleaved A/B, nt stores -1.5 % iteration, nt loads a
 // further -0.9 % (M1 then finds W still in the Infinity Cache).
@@ -252,7 +255,14 @@ void k5_fused(K5Args a) {
     // interleaved pairs, profiles/round4/ab_k5_one_layout.txt).
     constexpr int LDP = ((RP + 31) / 32) * 32 + 16;
     constexpr int SLICE = 16 * LDP + 16;
-    constexpr int NBUF = 4, SD = 2;
+#ifndef TRITD_K5_NBUF  // A/B builds only (round 6: the 3-waves-per-SIMD study)
+#define TRITD_K5_NBUF 4
+#endif
+#ifndef TRITD_K5_PF
+#define TRITD_K5_PF 1
+#endif
+    constexpr int NBUF = TRITD_K5_NBUF, SD = NBUF / 2;
+    constexpr bool PF = TRITD_K5_PF != 0;  // tile tt+1 prefetched into the second register set
     __shared__ __attribute__((aligned(16))) double sCS[NBUF][SLICE];
     auto slice_buf = [](int64_t s) { return (int)(s & (NBUF - 1)); };
     // per-wave 16x16 transpose buffer for T (stored in the M3 B-operand order)
@@ -420,7 +430,14 @@ void k5_fused(K5Args a) {
         const int64_t o = (tm_tile_base(tile, tt, ntt) >> 1) + lane;
         // prefetch first
         if (ps) stage_load(tt + SD);
-        if (pf) {
+        if (!PF) {  // (A/B: no register prefetch; other waves cover the latency)
+            load(tt, cx);
+            if constexpr (DE) {
+                load_dense(tt, cx);
+                load_dense_p(tt, cx);
+            }
+        }
+        if (pf && PF) {
             load(tt + 1, nx);
             if constexpr (DE) {  // both E tiles are part of the regular batch
                 load_dense(tt + 1, nx);
@@ -572,10 +589,12 @@ void k5_fused(K5Args a) {
     xa.ce = xb.ce = xa.cep = xb.cep = 0.0;
     load_slot(t0, xa);
     load_slot(t0 + 1, xb);
-    load(t0, xa);
-    if (DE) {
-        load_dense(t0, xa);
-        load_dense_p(t0, xa);
+    if (PF) {
+        load(t0, xa);
+        if (DE) {
+            load_dense(t0, xa);
+            load_dense_p(t0, xa);
+        }
     }
     for (int64_t q = 0; q < SD; ++q) {  // the first SD slices
         if (t0 + q < t1) {
@@ -588,13 +607,14 @@ void k5_fused(K5Args a) {
     // steps in pairs (the register sets alternate by name; every flag is a
     // constant inside the loop); with SD = 2 only the second step of a pair
     // ends at a barrier
+    // (SD = 1, A/B only: every step ends at a barrier)
     for (; tt + 3 < t1; tt += 2) {
-        body(tt, slice_buf(tt - t0), xa, xb, true, true, false);
+        body(tt, slice_buf(tt - t0), xa, xb, true, true, SD == 1);
         body(tt + 1, slice_buf(tt + 1 - t0), xb, xa, true, true, true);
     }
     {
         const int64_t rem = t1 - tt;  // 1..3 steps left
-        body(tt, slice_buf(tt - t0), xa, xb, rem > 1, rem > SD, false);
+        body(tt, slice_buf(tt - t0), xa, xb, rem > 1, rem > SD, SD == 1 && rem > 1);
         if (rem > 1) body(tt + 1, slice_buf(tt + 1 - t0), xb, xa, rem > 2, rem > 1 + SD, rem > 2);
         if (rem > 2) body(tt + 2, slice_buf(tt + 2 - t0), xa, xb, false, false, false);
     }
