@@ -591,7 +591,9 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=None, help="config 4: cube side override")
+    ap.add_argument("--n", "--side", dest="n", type=int, default=None,
+                    help="config 4: cube side override (--side under torchrun, whose own "
+                         "parser takes --n for an abbreviation of its options)")
     ap.add_argument("--r", type=int, default=None)
     # the full 100-iteration solve at configs 1-4 (one
     # iteration at config 5, reported per iteration)

@@ -93,3 +93,30 @@ def test_bench_two_ranks_from_plain_shell():
         assert p["allreduces_per_iteration"] == 2
         assert 0 < p["allreduce_ms"] < p["iteration_ms"]
         assert abs(p["compute_ms"] + p["allreduce_ms"] - p["iteration_ms"]) < 1e-9
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_under_torchrun():
+    """The driver's own N > 1 command shape (`python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus N ...`), 2 ranks sharing the box's GPU over the host
+    transport: torchrun's rank processes publish the rendezvous port over gloo
+    and run the GPU work in torch-free workers; the line reports one HIP / HSA
+    / RCCL copy each, from /opt/rocm, in rank 0's worker."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), BENCH, "--gpus", "2", "--comm", "host", "--no-cpu", "--no-e2e",
+                        "--side", "64", "--steps", "4", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=600, env=_env())
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["comm"] == {"transport": "host", "nranks": 2}
+    assert line["value"] > 0 and line["rre_final"] < 1e-3
+    st = line["runtime_stack"]
+    assert all(len(v) == 1 and v[0].startswith("/opt/rocm") for v in st.values()), st

@@ -12,8 +12,8 @@ n, r = 512, 8
 n1 = n2 = n3 = n
 if os.environ.get("AB_CFG", "4") == "5":  # 2048x2048x256 r=16 fp32 (bench.py --config 5)
     n1, n2, n3, r = 2048, 2048, 256, 16
-    dd = synth.low_rank_plus_outliers(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
-    D, A0, B0, C0 = dd["D"].astype(np.float32, order="F"), dd["A0"], dd["B0"], dd["C0"]
+    dd = synth.low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+    D, A0, B0, C0 = dd["D"], dd["A0"], dd["B0"], dd["C0"]
     del dd
 elif os.environ.get("AB_CFG", "4") == "3":  # 240x320x300 r=5 video stand-in (bench.py --config 3)
     n1, n2, n3, r = 240, 320, 300, 5
