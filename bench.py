@@ -144,6 +144,40 @@ def end_to_end(tritd, D, r, opts, A0, B0, C0, device):
         res[label] = {"ms": min(t), "ms_each": [round(x, 2) for x in t]}
     res["ms"] = res["default"]["ms"]
     res["probe_net_ms"] = res["with_probe"]["ms"] - res["default"]["ms"]
+    # where a one-shot call's time goes: the same steps
+    # through a session, each timed — create (D over PCIe, tile-major layout),
+    # the 100 device-resident iterations, get (fix-ups and layout on the
+    # device, then O, E, factors and errHist back over PCIe) — and the bare
+    # PCIe rate of one D-sized copy each way on this box
+    from tritd import hip
+    t0 = time.perf_counter()
+    s = tritd.Session(r, o, A0, B0, C0, n1=D.shape[0], n2=D.shape[1], n3=D.shape[2], D=D,
+                      device=device, probe=False)
+    t1 = time.perf_counter()
+    s.run(100)
+    s.sync()
+    t2 = time.perf_counter()
+    out = s.get()
+    t3 = time.perf_counter()
+    s.close()
+    del out
+    Df = np.asfortranarray(D)
+    buf = np.empty_like(Df)
+    hip.synchronize()
+    t4 = time.perf_counter()
+    dev = hip.DeviceArray.from_host(Df)  # (includes the hipMalloc of 1 GB)
+    hip.synchronize()
+    t5 = time.perf_counter()
+    dev.to_host(buf)  # (into pages the first touch must fault in)
+    t6 = time.perf_counter()
+    dev.free()
+    del buf
+    res["session_path"] = {"create_ms": (t1 - t0) * 1e3, "iterations_ms": (t2 - t1) * 1e3,
+                           "get_ms": (t3 - t2) * 1e3,
+                           "note": "tritd.Session(D host) / run(100) / get(): O, E, A, B, C, errHist"}
+    res["pcie"] = {"bytes": int(D.nbytes), "h2d_GBs": D.nbytes / (t5 - t4) / 1e9,
+                   "d2h_GBs": D.nbytes / (t6 - t5) / 1e9,
+                   "note": "one hipMemcpy of D each way from pageable host memory"}
     return res
 
 
