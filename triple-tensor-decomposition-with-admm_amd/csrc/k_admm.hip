@@ -218,7 +218,10 @@ void k5_fused(K5Args a) {
     }
     // workgroup wgi = chunk c of the t-walk (a.tsplit chunks; 1 unless the
     // problem has too few ij-tiles to fill the GPU, k5_tsplit) x group bid of
-    // 4 ij-tiles
+    // 4 ij-tiles.  (Round 6: one workgroup walking 2 or 4 such units in turn,
+    // bitwise the same results, measured K5 0.933 / 0.934 vs 0.919 ms —
+    // profiles/round6/k5_ab/ab_k5_units_per_workgroup_dropped.txt: the
+    // workgroup turnover is not where the per-walk fixed cost goes.)
     const int64_t wgi = (int64_t)blockIdx.x - side;
     const int64_t ngrp = (a.tiles + K5_WAVES - 1) / K5_WAVES;
     const int64_t chunk = wgi / ngrp;
