@@ -513,9 +513,11 @@ void run_group(const std::vector<int>& devs, const void* D, size_t es, uint32_t 
     const int P = grp.size();
     if (P == 1) {
         Session s(devs[0], D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, flags);
+        OutputPrefault pf(O, E, (size_t)(n1 * n2 * n3) * es);
         s.run(o.maxIter);
+        pf.join();
         int k = 0;
-        s.get(A, B, C, O, E, n1, errHist, &k);
+        s.get(A, B, C, O, E, n1, errHist, &k, true);
         g_last_flags |= s.flags();
         if (iters) *iters = k;
         return;
@@ -748,9 +750,11 @@ tritd_status tritd_admm_f64(const double* D, int64_t n1, int64_t n2, int64_t n3,
         }
         const int dev = pick_device(device < 0 && !g_devices.empty() ? g_devices[0] : device);
         Session s(dev, D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, 0);
+        OutputPrefault pf(O, E, (size_t)(n1 * n2 * n3) * sizeof(double));
         s.run(o.maxIter);
+        pf.join();
         int k = 0;
-        s.get(A, B, C, O, E, n1, errHist, &k);
+        s.get(A, B, C, O, E, n1, errHist, &k, true);
         g_last_flags |= s.flags();
         if (iters) *iters = k;
     });
@@ -774,9 +778,11 @@ tritd_status tritd_admm_f32(const float* D, int64_t n1, int64_t n2, int64_t n3, 
         }
         const int dev = pick_device(device < 0 && !g_devices.empty() ? g_devices[0] : device);
         Session s(dev, D, n1, n1, n2, n3, 0, n1, r, o, A0, B0, C0, nullptr, TRITD_SESSION_F32);
+        OutputPrefault pf(O, E, (size_t)(n1 * n2 * n3) * sizeof(float));
         s.run(o.maxIter);
+        pf.join();
         int k = 0;
-        s.get(A, B, C, O, E, n1, errHist, &k);
+        s.get(A, B, C, O, E, n1, errHist, &k, true);
         g_last_flags |= s.flags();
         if (iters) *iters = k;
     });

@@ -630,7 +630,21 @@ void Session::maybe_dense_e(int k) {
     de_ = true;
 }
 
-void populate_output(void* p, size_t bytes) {
+void populate_output(void* p, size_t bytes) { populate_output_threads(p, bytes, 16); }
+
+OutputPrefault::OutputPrefault(void* O, void* E, size_t bytes) {
+    if (O || E)
+        t_ = std::thread([O, E, bytes] {
+            if (O) populate_output_threads(O, bytes, 8);
+            if (E) populate_output_threads(E, bytes, 8);
+        });
+}
+
+void OutputPrefault::join() {
+    if (t_.joinable()) t_.join();
+}
+
+void populate_output_threads(void* p, size_t bytes, unsigned max_threads) {
     if (!p || bytes < ((size_t)64 << 20)) return;
 #ifndef MADV_POPULATE_WRITE
 #define MADV_POPULATE_WRITE 23  // Linux 5.14
@@ -647,7 +661,7 @@ void populate_output(void* p, size_t bytes) {
         if (he > ha) (void)madvise((void*)ha, (size_t)(he - ha), MADV_HUGEPAGE);
     }
     const unsigned hc = std::thread::hardware_concurrency();
-    const uintptr_t nt = std::min<uintptr_t>(16, hc ? hc : 1);
+    const uintptr_t nt = std::min<uintptr_t>(max_threads ? max_threads : 1, hc ? hc : 1);
     const uintptr_t chunk = (((e - a) / nt) + GR - 1) & ~(GR - 1);
     std::vector<std::thread> th;
     for (uintptr_t s = a; s < e; s += chunk) {
@@ -1262,7 +1276,7 @@ void Session::kernel_ms(double* k5, double* m3, double* it, int* samples) {
 }
 
 void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldOE,
-                  double* errHist, int* iters) {
+                  double* errHist, int* iters, bool populated) {
     int done = 0, stopped = 0;
     sync(&done, &stopped);
     if (A) {  // the A of the last finished iteration (its parity buffer)
@@ -1295,23 +1309,49 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
             launch_ce_expand(g_, ce_buf(done), e_buf(done), st_);
     }
     if ((O || E) && g_.n1l > 0) {
-        DBuf tmp;
-        tmp.alloc_bytes((size_t)(g_.n1l * g_.n2 * g_.n3) * es_);
+        // Round 6 (the drop-in's one-shot call): the host
+        // pages of both outputs are populated on two threads while the device
+        // rebuilds O, expands E and converts both to column-major, each into
+        // a buffer of its own; the D2H copies (PCIe, ~30 GB/s on the boxes
+        // measured: profiles/round6/pcie_probe.txt) then run back to back
+        // into pages that no longer fault.  (Fresh pages cost the copy a
+        // factor 2.5: 12.3 vs 30.2 GB/s.)
+        const size_t nb = (size_t)(g_.n1l * g_.n2 * g_.n3) * es_;
+        const bool whole = ldOE == g_.n1l;  // a whole tensor (one-shot calls): contiguous copies
+        std::vector<std::thread> pop;
+        if (whole && !populated)
+            for (void* dst : {O, E})
+                if (dst) pop.emplace_back([dst, nb] { populate_output_threads(dst, nb, 8); });
+        struct Join {
+            std::vector<std::thread>& t;
+            ~Join() {
+                for (auto& x : t)
+                    if (x.joinable()) x.join();
+            }
+        } join{pop};
+        DBuf tmp[2];
+        int q = 0;
         for (auto pr : {std::make_pair(O, O_.p), std::make_pair(E, e_buf(done))}) {
             if (!pr.first) continue;
+            tmp[q].alloc_bytes(nb);
             if (f32_)
-                launch_from_tm32(g_, reinterpret_cast<float*>(pr.second), tmp.f(), g_.n1l, st_);
+                launch_from_tm32(g_, reinterpret_cast<float*>(pr.second), tmp[q].f(), g_.n1l, st_);
             else
-                launch_from_tm(g_, pr.second, tmp.p, g_.n1l, st_);
-            if (ldOE == g_.n1l) {  // a whole tensor (one-shot calls): one contiguous copy
-                const size_t nb = (size_t)(g_.n1l * g_.n2 * g_.n3) * es_;
-                populate_output(pr.first, nb);
-                TRITD_HIP(hipMemcpyAsync(pr.first, tmp.p, nb, hipMemcpyDeviceToHost, st_));
-            } else
-                TRITD_HIP(hipMemcpy2DAsync(pr.first, ldOE * es_, tmp.p, g_.n1l * es_, g_.n1l * es_,
-                                           (size_t)(g_.n2 * g_.n3), hipMemcpyDeviceToHost, st_));
-            TRITD_HIP(hipStreamSynchronize(st_));
+                launch_from_tm(g_, pr.second, tmp[q].p, g_.n1l, st_);
+            ++q;
         }
+        for (auto& x : pop) x.join();
+        q = 0;
+        for (void* dst : {O, E}) {
+            if (!dst) continue;
+            if (whole)
+                TRITD_HIP(hipMemcpyAsync(dst, tmp[q].p, nb, hipMemcpyDeviceToHost, st_));
+            else
+                TRITD_HIP(hipMemcpy2DAsync(dst, ldOE * es_, tmp[q].p, g_.n1l * es_, g_.n1l * es_,
+                                           (size_t)(g_.n2 * g_.n3), hipMemcpyDeviceToHost, st_));
+            ++q;
+        }
+        TRITD_HIP(hipStreamSynchronize(st_));
     }
     if (errHist && done > 0)
         TRITD_HIP(hipMemcpy(errHist, errHist_.p, (size_t)done * sizeof(double), hipMemcpyDeviceToHost));

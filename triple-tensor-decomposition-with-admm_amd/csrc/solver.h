@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -32,6 +33,22 @@ namespace tritd {
 // it then runs at the single-threaded page-fault rate (~16 GB/s measured
 // against ~55 GB/s into populated memory).  No-op below 64 MB.
 void populate_output(void* p, size_t bytes);
+void populate_output_threads(void* p, size_t bytes, unsigned max_threads);
+
+// The one-shot calls' outputs O and E (whole tensors in the caller's memory)
+// faulted in on a background thread while the iterations run on the device:
+// a D2H copy into pages that fault runs at 12.6 instead of 30 GB/s
+// (profiles/round6/pcie_probe.txt), and populating them in get() took as long
+// as the copies.  join() before Session::get(..., populated = true).
+class OutputPrefault {
+public:
+    OutputPrefault(void* O, void* E, size_t bytes);
+    ~OutputPrefault() { join(); }
+    void join();
+
+private:
+    std::thread t_;
+};
 
 // In-place all-reduce (sum, or max) of `count` doubles over the comm's ranks,
 // ordered on stream st: ncclAllReduce, or the host transport (drains st).
@@ -85,9 +102,10 @@ class Session {
     void sync(int* done, int* stopped);
     // TRITD_FLAG_* raised by the device so far (read at every sync)
     uint32_t flags() const { return flags_; }
-    // O, E: double, or float for an fp32 session
+    // O, E: double, or float for an fp32 session.  populated: the caller has
+    // already faulted in the pages of whole-tensor O and E (OutputPrefault)
     void get(double* A, double* B, double* C, void* O, void* E, int64_t ldOE, double* errHist,
-             int* iters);
+             int* iters, bool populated = false);
     // dX: device tensor of the session's data type
     void rre_parts(const void* dX, int64_t ldX, double* num, double* den);
     bool is_f32() const { return f32_; }
