@@ -120,6 +120,24 @@ def test_f32_large_rank_vs_c_oracle(tritd, cref, shape, r, iters):
     _compare(tritd, cref, d["D"].astype(np.float32), r, opts, d["A0"], d["B0"], d["C0"])
 
 
+@pytest.mark.parametrize("P", [2, 3])
+def test_f32_r16_sharded_vs_c_oracle(tritd, cref, P):
+    """Config 5's rank (r = 16, padded rank 256) on the mode-1 sharded schedule
+     — what the config-5 leg of an N > 1 bench runs on every
+    rank: one GPU repeated P times as a device set (one host thread and one
+    session per shard, all-reduces in shard order), shards of 32 | 32 and
+    22 | 21 | 21 rows (straddling the 16-row tiles), against the C restatement
+    at the fp32 tolerances of this module."""
+    from tritd import synth
+    d = synth.low_rank_plus_outliers_f32(64, 64, 48, 16, p_out=0.05, seed=2, init_seed=7)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=10)
+    tritd.set_devices([0] * P)
+    try:
+        _compare(tritd, cref, d["D"], 16, opts, d["A0"], d["B0"], d["C0"])
+    finally:
+        tritd.set_devices([])
+
+
 @pytest.mark.timeout(300)
 def test_f32_r16_long_horizon_vs_c_oracle(tritd, cref, capsys):
     """Config 5's rank (r = 16, padded rank 256) over the whole 100-iteration

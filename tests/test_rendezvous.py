@@ -20,6 +20,7 @@ def _port():
 
 def _rank(rank, world, port, q, fail_rank):
     import sys
+    import numpy as np
     sys.path.insert(0, PKG)
     from tritd.rendezvous import StarGroup
     try:
@@ -30,6 +31,11 @@ def _rank(rank, world, port, q, fail_rank):
         out["max"] = g.allreduce_max(float(rank) * 1.5)
         out["sum"] = g.allreduce_sum([1.0, float(rank), 0.1 * rank])
         out["gather"] = g.allgather([rank, rank * rank])
+        a = np.arange(5, dtype=np.float64) * (rank + 1)
+        g.allreduce_f64(a)
+        b = np.array([rank, -rank, 0.5], dtype=np.float64)
+        g.allreduce_f64(b, "max")
+        out["f64"] = (a.tolist(), b.tolist())
         if rank == fail_rank:
             os._exit(3)  # dies without closing anything: the others must not hang
         g.barrier()
@@ -72,6 +78,8 @@ def test_star_group_collectives(world):
         assert out["sum"] == [float(world), float(sum(range(world))),
                               sum(0.1 * k for k in range(world))]
         assert out["gather"] == [[k, k * k] for k in range(world)]
+        tot = sum(k + 1 for k in range(world))
+        assert out["f64"] == ([float(i * tot) for i in range(5)], [world - 1.0, 0.0, 0.5])
 
 
 def test_star_group_peer_failure_does_not_hang():

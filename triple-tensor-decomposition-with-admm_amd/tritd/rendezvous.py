@@ -164,6 +164,45 @@ class StarGroup:
     def allgather(self, value):
         return self._exchange(value, list)
 
+    def allreduce_f64(self, buf, op="sum"):
+        """In-place sum (rank order) or max of a float64 numpy array over the
+        ranks, as raw bytes (the host transport's all-reduces: ~0.6 M doubles
+        per call at config 5, which JSON would turn into megabytes of text)."""
+        import numpy as np
+        self._seq += 1
+        if self.world == 1:
+            return buf
+        hdr = struct.Struct("<QQ")  # seq, nbytes
+        data = np.ascontiguousarray(buf, dtype=np.float64)
+
+        def send(sock, arr):
+            b = arr.tobytes()
+            sock.sendall(hdr.pack(self._seq, len(b)) + b)
+
+        def recv(sock):
+            deadline = time.monotonic() + self.timeout
+            seq, n = hdr.unpack(_recv_exact(sock, hdr.size, deadline))
+            if seq != self._seq or n != data.nbytes:
+                raise RuntimeError("rendezvous: peer out of step (%d/%d bytes %d/%d)"
+                                   % (seq, self._seq, n, data.nbytes))
+            return np.frombuffer(_recv_exact(sock, n, deadline), dtype=np.float64)
+
+        if self.rank == 0:
+            acc = data.copy()
+            for p in self.peers:
+                v = recv(p)
+                if op == "max":
+                    np.maximum(acc, v, out=acc)
+                else:
+                    acc += v
+            for p in self.peers:
+                send(p, acc)
+        else:
+            send(self.sock, data)
+            acc = recv(self.sock)
+        buf[...] = acc.reshape(buf.shape)
+        return buf
+
     def close(self):
         for p in self.peers:
             p.close()
@@ -183,15 +222,9 @@ def make_comm(group: StarGroup, device: int):
 def make_host_comm(group: StarGroup, device: int):
     """libtritd's host transport with the group's all-reduces (sum / max of
     float64 buffers): the multi-rank schedule with ranks sharing a GPU."""
-    import numpy as np
     from .api import Comm
 
     def fn(buf, op):
-        if op:
-            out = group._exchange([float(a) for a in buf],
-                                  lambda vs: [max(col) for col in zip(*vs)])
-        else:
-            out = group.allreduce_sum(buf)
-        buf[:] = np.asarray(out, dtype=np.float64)
+        group.allreduce_f64(buf, "max" if op else "sum")
 
     return Comm.host(fn, group.world, group.rank, device)
