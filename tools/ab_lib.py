@@ -17,7 +17,7 @@ for p in paths:
             continue
         fn = getattr(l, name); fn.restype = res; fn.argtypes = args
     libs[p] = l
-n, r = 512, 8
+n, r = 512, int(os.environ.get("AB_R", "8"))
 n1 = n2 = n3 = n
 cfg5 = os.environ.get("AB_CFG", "4") == "5"
 if cfg5:  # 2048x2048x256 r=16 fp32 (bench.py --config 5)
