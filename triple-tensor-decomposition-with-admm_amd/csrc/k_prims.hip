@@ -64,7 +64,12 @@ void launch_sumsq_padded(const Geom& g, const double* X, double* partial, int nb
 // barriers save); the factors read in their reference layouts (no pack
 // kernel) 358.5; no LDS at all — one wave per workgroup loading its operands
 // from L2 by buffer loads — 371.7, or 385.9 with the next t-tile's operands
-// prefetched (122 VGPRs); s_setprio(1) around the MFMA chain 337.6 vs 334.0.  (Round 3's form staged 32 t-values per step
+// prefetched (122 VGPRs); s_setprio(1) around the MFMA chain 337.6 vs 334.0.
+// Round 6: the two-tile form with each workgroup's t-chunk of C^T staged in LDS
+// once and no barrier in the walk (chunks of 2 / 4 / 8 / 16 t-tiles) ran 0.784
+// / 0.529 / 0.406 / 0.379 vs 0.342 ms, bitwise equal: the per-workgroup start
+// (Khatri-Rao gather, LDS fill) is what a t-chunk pays again, not the barriers
+// (profiles/round6/tp3_chunks_dropped.txt).  (Round 3's form staged 32 t-values per step
 // without double buffering, two barriers each: 0.464 ms.)
 // ---------------------------------------------------------------------------
 #ifndef TP_WV
