@@ -305,14 +305,23 @@ void k5_fused(K5Args a) {
     auto opL = [&](int buf, int s) { return sCS[buf][offL + 4 * s]; };
     auto opW = [&](int buf, int r, int m) { return sCS[buf][offW + r * (4 * LDP + 4) + 16 * m]; };
 
-    // the Khatri-Rao operand of this ij-tile: KR(ij, 4s+tg) (CP or Qi, kernels.h)
+    // the Khatri-Rao operand of this ij-tile: KR(ij, 4s+tg) (CP or Qi, kernels.h).
+    // Every load is unconditional and issued before the first product (an
+    // inactive wave's i = j = 0 is in range; its KR is zeroed by a select):
+    // loads guarded by `active` compiled to a branch and a vmcnt(0) wait per
+    // element — KS serial L2 round trips at the start of every workgroup
+    // (round 6).
     double kr[KS];
     if (!PRO) {
+        double av[KS], bv[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int k = 4 * s + tg;
-            kr[s] = active ? a.Ah[j * a.ahj + i * RP + k] * a.Bh[j * a.bhj + k] : 0.0;
+            av[s] = a.Ah[j * a.ahj + i * RP + k];
+            bv[s] = a.Bh[j * a.bhj + k];
         }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kr[s] = active ? av[s] * bv[s] : 0.0;
     }
     d4 wacc[MT];
 #pragma unroll

@@ -206,11 +206,16 @@ void k5_f32(K5Args32 a) {
 
     float kr[KS];  // L operand KR(ij = l & 15, k = (l>>4) * KS + s), single-rounded
     if (!PRO) {
+        // unconditional loads, all issued first (k_admm.hip: the KR gather)
+        double av[KS], bv[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int k = tg * KS + s;
-            kr[s] = active ? (float)(a.Ah[i * RP + k] * a.Bh[j * RP + k]) : 0.0f;
+            av[s] = a.Ah[i * RP + k];
+            bv[s] = a.Bh[j * RP + k];
         }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kr[s] = active ? (float)(av[s] * bv[s]) : 0.0f;
     }
     f4 wacc[MT];
 #pragma unroll

@@ -76,10 +76,17 @@ void k_als_fit(AlsFitArgs a) {
     };
 
     double kr[KS];  // (A^ o B^)(ij, 4s + l>>4): the Khatri-Rao row of this lane's ij
+    {
+        // unconditional loads, all issued first (k_admm.hip: the KR gather)
+        double av[KS], bv[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const int k = 4 * s + tg;
-        kr[s] = active ? a.Ah[i * RP + k] * a.Bh[j * RP + k] : 0.0;
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + tg;
+            av[s] = a.Ah[i * RP + k];
+            bv[s] = a.Bh[j * RP + k];
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kr[s] = active ? av[s] * bv[s] : 0.0;
     }
     d4 wacc[MT];
 #pragma unroll

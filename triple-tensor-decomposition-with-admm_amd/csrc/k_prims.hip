@@ -100,10 +100,17 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp(const double* __restrict__
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const bool row_ok = active && i < n1l;
     double kr[KS];
+    {
+        // unconditional loads, all issued first (k_admm.hip: the KR gather)
+        double av[KS], bv[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const int k = 4 * s + tg;
-        kr[s] = active ? Ah[j * ahj + i * RP + k] * Bh[j * bhj + k] : 0.0;  // kernels.h: KR source
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + tg;
+            av[s] = Ah[j * ahj + i * RP + k];  // kernels.h: KR source
+            bv[s] = Bh[j * bhj + k];
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kr[s] = active ? av[s] * bv[s] : 0.0;
     }
     const int64_t ntt = n3p >> 4;
     d2v sv[NS];
@@ -210,12 +217,22 @@ __global__ __launch_bounds__(64 * TP_WAVES) void k_tp2(const double* __restrict_
     const int64_t j = active ? tile0 / qper : 0;
     const int64_t i0 = active ? (tile0 - j * qper) << 4 : 0;  // first i of the 32
     double kr0[KS], kr1[KS];
+    {
+        // unconditional loads, all issued first (k_admm.hip: the KR gather;
+        // an inactive wave reads rows 0..31, in range since qper is even)
+        double a0[KS], a1[KS], bv[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const int k = 4 * s + tg;
-        const double b = active ? Bh[j * bhj + k] : 0.0;
-        kr0[s] = active ? Ah[j * ahj + (i0 + il) * RP + k] * b : 0.0;
-        kr1[s] = active ? Ah[j * ahj + (i0 + 16 + il) * RP + k] * b : 0.0;
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + tg;
+            bv[s] = Bh[j * bhj + k];
+            a0[s] = Ah[j * ahj + (i0 + il) * RP + k];
+            a1[s] = Ah[j * ahj + (i0 + 16 + il) * RP + k];
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            kr0[s] = active ? a0[s] * bv[s] : 0.0;
+            kr1[s] = active ? a1[s] * bv[s] : 0.0;
+        }
     }
     const int64_t ntt = n3p >> 4;
     d2v sv[NS];
