@@ -222,10 +222,12 @@ void k5_fused(K5Args a) {
     // bitwise the same results, measured K5 0.933 / 0.934 vs 0.919 ms —
     // profiles/round6/k5_ab/ab_k5_units_per_workgroup_dropped.txt: the
     // workgroup turnover is not where the per-walk fixed cost goes.)
-    const int64_t wgi = (int64_t)blockIdx.x - side;
-    const int64_t ngrp = (a.tiles + K5_WAVES - 1) / K5_WAVES;
-    const int64_t chunk = wgi / ngrp;
-    const int64_t bid = wgi - chunk * ngrp;  // this workgroup's group of ij-tiles
+    // (index arithmetic in 32 bits: every count here is far below 2^32, and
+    // a 64-bit division is ~100 scalar instructions of every workgroup's start)
+    const uint32_t wgi = blockIdx.x - (uint32_t)side;
+    const uint32_t ngrp = (uint32_t)((a.tiles + K5_WAVES - 1) / K5_WAVES);
+    const uint32_t chunk = wgi / ngrp;
+    const uint32_t bid = wgi - chunk * ngrp;  // this workgroup's group of ij-tiles
     WT_BEGIN();
     constexpr int KS = RP / 4;   // MFMA K-steps for L
     constexpr int MT = RP / 16;  // k-tiles of W
@@ -235,13 +237,14 @@ void k5_fused(K5Args a) {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int il = lane & 15;
     const int tg = lane >> 4;
-    const int64_t tile = bid * K5_WAVES + wid;
+    const int64_t tile = (int64_t)bid * K5_WAVES + wid;
     const bool active = tile < a.tiles;
-    const int64_t qper = a.n1p >> 4;
-    const int64_t j = active ? tile / qper : 0;
+    const uint32_t qper = (uint32_t)(a.n1p >> 4);
+    const int64_t j = active ? (uint32_t)tile / qper : 0;
     const int64_t i = active ? ((tile - j * qper) << 4) + il : 0;
     const int64_t ntt = a.ntt;
-    const int64_t t0 = chunk * ntt / a.tsplit, t1 = (chunk + 1) * ntt / a.tsplit;  // this chunk's t-tiles
+    const int64_t t0 = chunk * (uint32_t)ntt / (uint32_t)a.tsplit;  // this chunk's t-tiles
+    const int64_t t1 = (chunk + 1) * (uint32_t)ntt / (uint32_t)a.tsplit;
 
     // C^ rows of one t-tile, staged once per workgroup in ONE layout read by
     // both MFMA chains: element (t, k) at t*LDP + 2*(t>>1) + k, LDP = 16 mod
@@ -280,49 +283,36 @@ void k5_fused(K5Args a) {
     d2v sv[NS];
     // C^ slices through one descriptor: slice tt at a scalar offset
     const __amdgpu_buffer_rsrc_t rCh = wave_rsrc(a.Ch, (int)(a.n3p * RP * 8));
-    auto stage_load = [&](int64_t tt) {
+    auto stage_load_to = [&](int64_t tt, d2v (&dst)[NS]) {
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int e = threadIdx.x + q * 64 * K5_WAVES;
             if (SP % (64 * K5_WAVES) == 0 || e < SP)
-                sv[q] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rCh, 16 * e, (int)(tt * 16 * RP * 8), 0));
+                dst[q] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rCh, 16 * e, (int)(tt * 16 * RP * 8), 0));
         }
     };
-    auto stage_store = [&](int buf) {
+    auto stage_store_from = [&](int buf, const d2v (&src)[NS]) {
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int e = threadIdx.x + q * 64 * K5_WAVES;
             if (SP % (64 * K5_WAVES) == 0 || e < SP) {
                 const int row = (2 * e) / RP, k = (2 * e) % RP;
-                *reinterpret_cast<d2v*>(&sCS[buf][row * LDP + 2 * (row >> 1) + k]) = sv[q];
+                *reinterpret_cast<d2v*>(&sCS[buf][row * LDP + 2 * (row >> 1) + k]) = src[q];
             }
         }
     };
+    auto stage_load = [&](int64_t tt) { stage_load_to(tt, sv); };
+    auto stage_store = [&](int buf) { stage_store_from(buf, sv); };
     // operand reads: L (t = il, k = 4s+tg) and W (t = 4r+tg, k = 16m+il)
     const int offL = il * LDP + 2 * (il >> 1) + tg;
     const int offW = tg * LDP + 2 * (tg >> 1) + il;
     auto opL = [&](int buf, int s) { return sCS[buf][offL + 4 * s]; };
     auto opW = [&](int buf, int r, int m) { return sCS[buf][offW + r * (4 * LDP + 4) + 16 * m]; };
 
-    // the Khatri-Rao operand of this ij-tile: KR(ij, 4s+tg) (CP or Qi, kernels.h).
-    // Every load is unconditional and issued before the first product (an
-    // inactive wave's i = j = 0 is in range; its KR is zeroed by a select):
-    // loads guarded by `active` compiled to a branch and a vmcnt(0) wait per
-    // element — KS serial L2 round trips at the start of every workgroup
-    // (round 6).
+    // the Khatri-Rao operand of this ij-tile: KR(ij, 4s+tg) (CP or Qi,
+    // kernels.h), gathered in the prologue below
     double kr[KS];
-    if (!PRO) {
-        double av[KS], bv[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int k = 4 * s + tg;
-            av[s] = a.Ah[j * a.ahj + i * RP + k];
-            bv[s] = a.Bh[j * a.bhj + k];
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s) kr[s] = active ? av[s] * bv[s] : 0.0;
-    }
     d4 wacc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) wacc[m] = d4{0.0, 0.0, 0.0, 0.0};
@@ -599,6 +589,19 @@ void k5_fused(K5Args a) {
     xa.ed[0] = xa.ed[1] = xb.ed[0] = xb.ed[1] = d2v{0.0, 0.0};
     xa.edp[0] = xa.edp[1] = xb.edp[0] = xb.edp[1] = d2v{0.0, 0.0};
     xa.ce = xb.ce = xa.cep = xb.cep = 0.0;
+    // Prologue, in issue order: the first SD C^ slices (L2), the first tile
+    // and slots (HBM), then the Khatri-Rao gather (L2).  vmcnt is in order,
+    // so the slices' LDS writes wait for the slices only, and no L2 round
+    // trip is waited for before the HBM loads are in flight.  Every KR load
+    // is unconditional (an inactive wave's i = j = 0 is in range; its KR is
+    // zeroed by a select): loads guarded by `active` compiled to a branch and
+    // a vmcnt(0) wait per element, KS serial L2 round trips at the start of
+    // every workgroup (round 6).
+    static_assert(SD >= 1 && SD <= 2, "k5_fused: the prologue stages at most two slices");
+    d2v sv1[NS];
+    const bool st0 = t0 < t1, st1 = SD > 1 && t0 + 1 < t1;
+    if (st0) stage_load_to(t0, sv);
+    if (st1) stage_load_to(t0 + 1, sv1);
     load_slot(t0, xa);
     load_slot(t0 + 1, xb);
     if (PF) {
@@ -608,13 +611,23 @@ void k5_fused(K5Args a) {
             load_dense_p(t0, xa);
         }
     }
-    for (int64_t q = 0; q < SD; ++q) {  // the first SD slices
-        if (t0 + q < t1) {
-            stage_load(t0 + q);
-            stage_store(slice_buf(q));
+    double av[KS], bv[KS];
+    if (!PRO) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + tg;
+            av[s] = a.Ah[j * a.ahj + i * RP + k];
+            bv[s] = a.Bh[j * a.bhj + k];
         }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    if (st0) stage_store_from(slice_buf(0), sv);
+    if (st1) stage_store_from(slice_buf(1), sv1);
     __syncthreads();
+    if (!PRO) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kr[s] = active ? av[s] * bv[s] : 0.0;
+    }
     int64_t tt = t0;
     // steps in pairs (the register sets alternate by name; every flag is a
     // constant inside the loop); with SD = 2 only the second step of a pair
