@@ -148,9 +148,21 @@ void run_shard_threads(int P, Body&& body, AbortAll&& abort_all) {
         }
     };
     std::vector<std::thread> th;
-    for (int p = 1; p < P; ++p) th.emplace_back(run, p);
-    run(0);
+    th.reserve(P > 1 ? (size_t)(P - 1) : 0);
+    // a thread that cannot be started fails the call: the shards already
+    // running are released from their collectives and joined first
+    std::exception_ptr spawn_err;
+    for (int p = 1; p < P && !spawn_err; ++p) {
+        try {
+            th.emplace_back(run, p);
+        } catch (...) {
+            spawn_err = std::current_exception();
+            abort_all();
+        }
+    }
+    if (!spawn_err) run(0);
     for (auto& t : th) t.join();
+    if (spawn_err) std::rethrow_exception(spawn_err);
     for (int p = 0; p < P; ++p)
         if (err[(size_t)p]) std::rethrow_exception(err[(size_t)p]);
 }

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <system_error>
 #include <thread>
 
 namespace tritd {
@@ -633,11 +634,14 @@ void Session::maybe_dense_e(int k) {
 void populate_output(void* p, size_t bytes) { populate_output_threads(p, bytes, 16); }
 
 OutputPrefault::OutputPrefault(void* O, void* E, size_t bytes) {
-    if (O || E)
+    if (!O && !E) return;
+    try {  // an optimisation only: no thread, no prefault (get() faults the pages in)
         t_ = std::thread([O, E, bytes] {
             if (O) populate_output_threads(O, bytes, 8);
             if (E) populate_output_threads(E, bytes, 8);
         });
+    } catch (const std::system_error&) {
+    }
 }
 
 void OutputPrefault::join() {
@@ -664,9 +668,14 @@ void populate_output_threads(void* p, size_t bytes, unsigned max_threads) {
     const uintptr_t nt = std::min<uintptr_t>(max_threads ? max_threads : 1, hc ? hc : 1);
     const uintptr_t chunk = (((e - a) / nt) + GR - 1) & ~(GR - 1);
     std::vector<std::thread> th;
+    th.reserve((size_t)((e - a + chunk - 1) / chunk));
     for (uintptr_t s = a; s < e; s += chunk) {
         const size_t len = (size_t)std::min(chunk, e - s);
-        th.emplace_back([s, len] { (void)madvise((void*)s, len, MADV_POPULATE_WRITE); });
+        try {
+            th.emplace_back([s, len] { (void)madvise((void*)s, len, MADV_POPULATE_WRITE); });
+        } catch (const std::system_error&) {  // no thread to spare: this piece on the caller's
+            (void)madvise((void*)s, len, MADV_POPULATE_WRITE);
+        }
     }
     for (auto& t : th) t.join();
 }
@@ -1319,9 +1328,7 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
         const size_t nb = (size_t)(g_.n1l * g_.n2 * g_.n3) * es_;
         const bool whole = ldOE == g_.n1l;  // a whole tensor (one-shot calls): contiguous copies
         std::vector<std::thread> pop;
-        if (whole && !populated)
-            for (void* dst : {O, E})
-                if (dst) pop.emplace_back([dst, nb] { populate_output_threads(dst, nb, 8); });
+        pop.reserve(2);
         struct Join {
             std::vector<std::thread>& t;
             ~Join() {
@@ -1329,6 +1336,14 @@ void Session::get(double* A, double* B, double* C, void* O, void* E, int64_t ldO
                     if (x.joinable()) x.join();
             }
         } join{pop};
+        if (whole && !populated)
+            for (void* dst : {O, E})
+                if (dst) {
+                    try {  // (an optimisation: without the thread the copy faults the pages in)
+                        pop.emplace_back([dst, nb] { populate_output_threads(dst, nb, 8); });
+                    } catch (const std::system_error&) {
+                    }
+                }
         DBuf tmp[2];
         int q = 0;
         for (auto pr : {std::make_pair(O, O_.p), std::make_pair(E, e_buf(done))}) {
