@@ -125,6 +125,7 @@ struct IterScalars {
     double invL_next;    // 1/muL of the next iteration (fused T formation, :33)
     double muO_prev;     // muO of the previous iteration (derived Y_O, k_admm.hip)
     double rden;         // 1/den, correctly rounded (K5's division by den, k_admm.hip)
+    double cprev;        // invO * muO_prev (K5's R1 + R2 and R3 through E^(k) - E^(k-1), k_admm.hip)
 };
 
 // first double of tile (g, tt) in the tile-major layout

@@ -508,17 +508,21 @@ void k5_fused(K5Args a) {
                     // The statements of :41-53 with their multiply-adds fused
                     // and O formed as (R1 + R2)/2 (muL == muO, :16-17,56-57, so
                     // (muL R1 + muO R2)/(muL + muO) is exactly that average);
-                    // 18 f64 operations per element instead of 27 (K5 is
+                    // 17 f64 operations per element instead of 27 (K5 is
                     // bound by the SIMD issue its MFMAs share).
                     // Values agree with MATLAB's separate operators to
                     // rounding (the parity tolerances of DESIGN.md §2).
                     // Y_O^(k) = Y_L^(k) - muO_k (E^(k) - E^(k-1))  (derived Y_O)
+                    // With Y_O = Y_L - muO_prev dE (dE = E^(k) - E^(k-1)) and
+                    // invL = invO: R1 + R2 = (D - L) + invL Y_L + E - invO Y_O
+                    // = dL + E + cprev dE (cprev = invO muO_prev) and R3 = On +
+                    // invO Y_O = On + invO Y_L - cprev dE — 7 f64 operations
+                    // for :41-46 instead of 8 through Y_O (round 6: K5 0.922 ->
+                    // 0.915 ms, profiles/round6/k5_chain_dE_ab.txt)
                     const double dL = d - L;
-                    const double yo = fma(-sc.muO_prev, e - evp[r], yl);
-                    const double R1 = fma(sc.invL, yl, dL);                 // :41
-                    const double R2 = fma(-sc.invO, yo, e);                 // :42
-                    const double On = (R1 + R2) * 0.5;                      // :43
-                    const double R3 = fma(sc.invO, yo, On);                 // :46
+                    const double dE = e - evp[r];
+                    const double On = (dL + fma(sc.cprev, dE, e)) * 0.5;        // :41-43
+                    const double R3 = fma(-sc.cprev, dE, fma(sc.invO, yl, On));  // :46
                     // sign(R3).*max(abs(R3)-thr,0) as R3 - clamp(R3,-thr,thr)
                     // (thr >= 0): |R3| > thr gives R3 -/+ thr, the same rounded
                     // difference; otherwise a zero; NaN and Inf pass through

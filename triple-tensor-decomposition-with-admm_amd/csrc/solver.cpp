@@ -370,6 +370,7 @@ IterScalars Session::scalars(int k) const {
     s.rden = 1.0 / s.den;
     s.invL_next = 1.0 / mu_[(size_t)k];
     s.muO_prev = k >= 2 ? mu_[(size_t)k - 2] : 0.0;  // E^(0) = E^(-1) = 0: any value
+    s.cprev = s.invO * s.muO_prev;
     return s;
 }
 
