@@ -518,7 +518,9 @@ void k5_fused(K5Args a) {
                     // = dL + E + cprev dE (cprev = invO muO_prev) and R3 = On +
                     // invO Y_O = On + invO Y_L - cprev dE — 7 f64 operations
                     // for :41-46 instead of 8 through Y_O (round 6: K5 0.922 ->
-                    // 0.915 ms, profiles/round6/k5_chain_dE_ab.txt)
+                    // 0.915 ms, profiles/round6/k5_chain_dE_ab.txt).  (Starting
+                    // the L MFMA chain from D with -KR, so that it leaves D - L,
+                    // measured slower: 0.912 -> 0.923 ms, k5_dL_mfma_dropped.txt.)
                     const double dL = d - L;
                     const double dE = e - evp[r];
                     const double On = (dL + fma(sc.cprev, dE, e)) * 0.5;        // :41-43
