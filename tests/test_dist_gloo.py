@@ -46,9 +46,9 @@ def _worker(rank, world, port, name, outdir, kind="admm"):
     from tritd.dist import shard_bounds
     import tritd_sharded
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file store in the test's directory: no TCP port to race for (`port` unused)
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "gloo_store"),
+                            rank=rank, world_size=world)
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     import json
     opts = json.loads(str(z["opts"]))
@@ -118,9 +118,9 @@ def _lib_worker(rank, world, port, n1, stop, clear_tail, outdir):
     from tritd.dist import shard_bounds
     import tritd_sharded
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file store in the test's directory: no TCP port to race for (`port` unused)
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "gloo_store"),
+                            rank=rank, world_size=world)
     d, opts = _lib_case(n1, stop)
     i0, i1 = shard_bounds(n1, world, rank)
 

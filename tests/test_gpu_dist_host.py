@@ -23,14 +23,6 @@ from conftest import ORACLE, PKG, load_golden, rel
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _case(n1, stop, disp=False):
     from tritd import synth
     d = synth.low_rank_plus_outliers(n1, 10, 8, 2, seed=5, init_seed=9)
@@ -38,7 +30,7 @@ def _case(n1, stop, disp=False):
     return d, opts
 
 
-def _worker(rank, world, port, spec, outdir):
+def _worker(rank, world, spec, outdir):
     import sys
     for p in (PKG, ORACLE):
         sys.path.insert(0, p)
@@ -46,14 +38,34 @@ def _worker(rank, world, port, spec, outdir):
     from tritd.dist import shard_bounds
     if spec.get("rdzv"):  # bench.py's torch-free path (tritd.rendezvous)
         from tritd.rendezvous import StarGroup, make_host_comm as rz_host_comm
-        group = StarGroup(rank, world, port, timeout=120)
+        # rank 0 binds its own port and publishes it through a file (a port
+        # probed by the parent and bound later can be taken in between)
+        pf = os.path.join(outdir, "rdzv_port")
+        if rank == 0:
+            ls = socket.socket()
+            ls.bind(("127.0.0.1", 0))
+            ls.listen(world)
+            with open(pf + ".tmp", "w") as f:
+                f.write(str(ls.getsockname()[1]))
+            os.replace(pf + ".tmp", pf)
+            group = StarGroup(0, world, 0, listen_fd=ls.detach(), timeout=120)
+        else:
+            import time
+            t0 = time.monotonic()
+            while not os.path.exists(pf):
+                if time.monotonic() - t0 > 120:
+                    raise TimeoutError("rank 0 did not publish its port")
+                time.sleep(0.05)
+            with open(pf) as f:
+                group = StarGroup(rank, world, int(f.read()), timeout=120)
         dist = None
     else:
+        import datetime
         import torch.distributed as dist
         from tritd.dist import make_host_comm
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # a file store: no TCP port to race for
+        dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "gloo_store"),
+                                rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     kind = spec["kind"]
     if "golden" in spec:
         z = load_golden(spec["golden"])
@@ -92,12 +104,11 @@ def _run(tmp_path, world, spec):
     # gloo, this test process does not (it stays on /opt/rocm's HIP runtime)
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(q, world, port, spec, str(tmp_path))) for q in range(world)]
+    ps = [ctx.Process(target=_worker, args=(q, world, spec, str(tmp_path))) for q in range(world)]
     for p in ps:
         p.start()
     for p in ps:
-        p.join(200)
+        p.join(150)
     for p in ps:
         if p.is_alive():
             p.terminate()
