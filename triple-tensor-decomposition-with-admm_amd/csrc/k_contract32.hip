@@ -225,6 +225,8 @@ constexpr int M3W = 4;
 static int64_t m3_jchunks(const Geom& g) {
     const int64_t ntg = cdiv(g.ntt, 4), qper = g.n1p >> 4;
     int64_t jc = 2048 / (ntg * qper);
+    // (round 6, three workgroups per CU: 3 / 6 chunks instead of 4 measured
+    // slower, profiles/round6/c5_k2_ab.txt)
     if (jc < 1) jc = 1;
     if (jc > g.n2) jc = g.n2;
     return jc;
@@ -261,19 +263,33 @@ __global__ __launch_bounds__(64 * M3W) void k_m3_32(const float* __restrict__ T,
     constexpr int KSZ = V ? 16 * 16 * PITCH : 16 * KP;
     __shared__ __attribute__((aligned(16))) float krs[2][KSZ];
     // this thread's KR elements: e = threadIdx.x + 256 u -> (row e / RP, col e % RP)
+    // (RP == 64 M3W, config 5: element u of thread x is (row u, k = x): one
+    // B^ value per j and the 16 LDS writes at immediate offsets from one
+    // address — the general form kept 24 VGPRs of per-u addresses live: 176
+    // -> 148 VGPRs, three workgroups per CU instead of two, K2 4.94 -> 4.60 ms,
+    // profiles/round6/c5_k2_ab.txt)
+    constexpr bool ONEK = 64 * M3W == RP;
     double ah[PER > 0 ? PER : 1];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int e = threadIdx.x + 64 * M3W * u;
-        ah[u] = Ah[(q * 16 + e / RP) * RP + e % RP];
+        ah[u] = ONEK ? Ah[(q * 16 + u) * RP + threadIdx.x] : Ah[(q * 16 + e / RP) * RP + e % RP];
     }
     auto form = [&](int64_t j, int buf) {
+        if constexpr (ONEK) {
+            const int k = threadIdx.x;
+            const double bh = Bh[j * RP + k];
+            float* dst = &krs[buf][V ? (k & 15) * PITCH + (k >> 4) : k];
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int e = threadIdx.x + 64 * M3W * u;
-            const int row = e / RP, k = e % RP;
-            const int at = V ? (row * 16 + (k & 15)) * PITCH + (k >> 4) : row * KP + k;
-            krs[buf][at] = (float)(ah[u] * Bh[j * RP + k]);
+            for (int u = 0; u < PER; ++u) dst[u * (V ? 16 * PITCH : KP)] = (float)(ah[u] * bh);
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = threadIdx.x + 64 * M3W * u;
+                const int row = e / RP, k = e % RP;
+                const int at = V ? (row * 16 + (k & 15)) * PITCH + (k >> 4) : row * KP + k;
+                krs[buf][at] = (float)(ah[u] * Bh[j * RP + k]);
+            }
         }
     };
     f4 acc[MT];
