@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 6: config-5 K5 storing W with 16-B stores (a quarter of the store instructions) — fp32 parity
+# with the variant library, interleaved A/B at config 5.
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r6_wst; mkdir -p $O
+TRITD_LIB=$PWD/ab6/wst.so timeout -k 10 900 python3 -u -m pytest -x -v --timeout 800 --timeout-method thread -m gpu \
+    tests/test_gpu_f32.py tests/test_gpu_fullsize.py tests/test_gpu_determinism.py -k "f32 or config5" > $O/parity.txt 2>&1
+AB_CFG=5 timeout -k 10 600 python3 -u tools/ab_lib.py ab6/base.so,ab6/wst.so 3 6 > $O/ab_c5.txt 2>&1
+echo done

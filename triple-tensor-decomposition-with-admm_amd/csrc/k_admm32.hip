@@ -746,17 +746,22 @@ void k5_f32s(K5Args32 a) {
         walk(std::integral_constant<int, 0>{});
     __syncthreads();
     {
-        // two adjacent ij-tiles = 32 consecutive ij: each lane half of a wave
-        // stores one 128 B row piece of a k-plane
+        // two adjacent ij-tiles = 32 consecutive ij: one 128 B row piece of
+        // each k-plane
         const int64_t t0 = (int64_t)blockIdx.x * 2;
-        const int sl = (lane >> 4) & 1;
-        const bool ok = t0 + sl < a.tiles;
         float* wl = &sC[0][0];
-        float* dst = a.Wk + (t0 << 4) + 16 * sl + il;
-#pragma unroll 4
-        for (int k0 = 2 * wid; k0 < RP; k0 += 8) {
-            const int k = k0 + (lane >> 5);
-            if (ok) dst[(int64_t)k * a.plane] = wl[sl * WS + k * 16 + il];
+        // 16-B stores: 8 lanes per 128 B row piece, 8 k-rows per instruction
+        // (a quarter of the store instructions of the 4-B form: round 6, K5
+        // 13.45 -> 13.29 ms, profiles/round6/c5_w_store16_ab.txt)
+        const int qq = lane & 7;
+        const int sl = qq >> 2, c4 = (qq & 3) * 4;
+        const bool ok = t0 + sl < a.tiles;
+        float* dst = a.Wk + (t0 << 4) + 16 * sl + c4;
+#pragma unroll 2
+        for (int k0 = 8 * wid; k0 < RP; k0 += 32) {
+            const int k = k0 + (lane >> 3);
+            const f4 v = *reinterpret_cast<const f4*>(&wl[sl * WS + k * 16 + c4]);
+            if (ok) *reinterpret_cast<f4*>(dst + (int64_t)k * a.plane) = v;
         }
     }
     if (hrole == 0 && ndense && lane == 0)
