@@ -14,7 +14,12 @@ paths = sys.argv[1].split(",")
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 r = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 12
-d = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
+n1 = n2 = n3 = n
+if os.environ.get("AB_CFG", "4") == "5":  # 2048x2048x256 r=16 fp32 (bench.py --config 5)
+    n1, n2, n3, r = 2048, 2048, 256, 16
+    d = synth.low_rank_plus_outliers_f32(n1, n2, n3, r, p_out=0.05, seed=0, init_seed=123)
+else:
+    d = synth.low_rank_plus_outliers(n, n, n, r, p_out=0.05, seed=0, init_seed=123)
 opts = dict(synth.TRAFFIC_OPTS, maxIter=iters)
 ref = None
 for p in paths:
@@ -23,7 +28,7 @@ for p in paths:
         if hasattr(l, name):
             fn = getattr(l, name); fn.restype = res; fn.argtypes = args
     api.lib = _lib.lib = l
-    s = tritd.Session(r, opts, d["A0"], d["B0"], d["C0"], n1=n, n2=n, n3=n, D=d["D"], device=0,
+    s = tritd.Session(r, opts, d["A0"], d["B0"], d["C0"], n1=n1, n2=n2, n3=n3, D=d["D"], device=0,
                       probe=False)
     s.run(iters); s.sync()
     out = s.get()
