@@ -387,12 +387,21 @@ struct DeviceGroup {
             launch_vsum(const_cast<double* const*>(buf.data()), P, count, vst);
             return;
         }
+        // a hipSetDevice failure inside the group is recorded, not thrown, so
+        // that the group is always closed (as in group_comms)
+        hipError_t he = hipSuccess;
         ncclResult_t rr = ncclGroupStart();
         for (int p = 0; p < P && rr == ncclSuccess; ++p) {
-            TRITD_HIP(hipSetDevice(devs[p]));
+            he = hipSetDevice(devs[p]);
+            if (he != hipSuccess) {
+                (void)hipGetLastError();
+                break;
+            }
             rr = ncclAllReduce(buf[p], buf[p], (size_t)count, ncclFloat64, ncclSum, g_comms[p], st[p]);
         }
         ncclResult_t re = ncclGroupEnd();
+        if (he != hipSuccess)
+            throw Error(TRITD_ERR_HIP, std::string("hipSetDevice (grouped all-reduce): ") + hipGetErrorString(he));
         if (rr == ncclInProgress) rr = ncclSuccess;  // non-blocking communicators (group_comms)
         if (re == ncclInProgress) re = ncclSuccess;
         for (int p = 0; p < P && rr == ncclSuccess && re == ncclSuccess; ++p) re = nccl_settle(g_comms[p]);
