@@ -133,3 +133,20 @@ def test_repeated_solves_are_bitwise_identical(tritd, name):
     for other in runs[1:]:
         for a, b in zip(runs[0], other):
             np.testing.assert_array_equal(a, b)
+
+
+# solve A of iteration k+1 runs beside K5 of iteration k, before
+# k's stop test; the pinv fallback of that solve (and its flag) must wait for
+# apply A, which runs only if the loop goes on.  With maxIter = 0 the loop
+# stops before update_A(1), whose Gram (B0, C0 of the ill-conditioned case) is
+# singular: MATLAB performs no pinv, so no flag.  Both the MFMA apply (fp64,
+# r = 3) and the generic apply (single class) paths.
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_no_pinv_flag_for_an_update_the_loop_never_runs(tritd, dtype):
+    from tritd import _lib, synth
+    X, r, A0, B0, C0 = ill_conditioned(1000.0)
+    opts = dict(synth.TRAFFIC_OPTS, maxIter=0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", tritd.PinvToleranceWarning)
+        tritd.triple_decomp_ADMM(np.asfortranarray(X, dtype=dtype), r, opts, A0, B0, C0)
+    assert (_lib.lib.tritd_last_flags() & _lib.FLAG_PINV_TOL) == 0
